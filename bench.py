@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: agent-steps/s of SwarmACB-Homing-v0 (dandelion) on MI355X.
+
+Workload (BASELINE.json configs[1]): SwarmACB-Homing-v0,
+dandelion variant (24-D obs, continuous wheels), 20 e-pucks x 4096 envs per
+GPU, Isaac-profile step semantics, in-kernel Philox packet loss. Actions are
+the ML-Agents initial policy N(0,1) -> clamp(-3,3)/3 per wheel, drawn once per
+decision (decision period 5) and held for the 5 env.steps of the decision,
+which run as ONE fused kernel launch (every substep still integrates, resolves
+contacts, computes rewards/time-outs/auto-reset and writes the 24-D
+observation). All actions are generated in HBM before the timed region.
+
+One "step" = one env.step (physics update) of all envs on all GPUs; an
+agent-step = one robot advanced by one such step (the reference's own SPS
+counts agent-decisions = agent-steps / 5). Multi-GPU: one process per GPU
+(torchrun), envs sharded by global index (weak scaling), no collective in the
+data path; value = all agent-steps / max-over-ranks time.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(ROOT, "swarmacb-isaaclab_amd")
+for _p in (ROOT, PKG_DIR):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+METRIC = "agent-steps/sec (20 e-pucks × num_envs) SwarmACB-Homing-v0 at 1/2/4/8 MI355X"
+ALGO_BYTES_PER_AGENT_STEP = 129.0   # read x,y,yaw+action 20 B, write x,y,yaw+obs 108 B, ~1 B counters
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+N_AGENTS = 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1200, help="timed env.steps (physics updates)")
+    ap.add_argument("--warmup", type=int, default=50, help="untimed env.steps")
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--decision-period", type=int, default=5)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
+    return ap.parse_args()
+
+
+def cpu_baseline(budget_s: float, envs: int) -> dict | None:
+    """Reference-equivalent CPU step (the C restatement in oracle/, 1 thread) on a bounded sample."""
+    if budget_s <= 0:
+        return None
+    import numpy as np
+
+    from oracle import oracle as O
+
+    O.build()
+    E = min(envs, 1024)
+    env = O.OracleEnv("homing", "isaac", E, N_AGENTS, 24, False, 1200)
+    O.seed(0)
+    env.reset_all()
+    rng = np.random.default_rng(0)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        a = (np.clip(rng.normal(size=(E, N_AGENTS, 2)), -3, 3) / 3).astype(np.float32)
+        for _ in range(5):
+            env.step(a)
+            steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": E * N_AGENTS * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/swarm_oracle.c (C restatement of the reference step, pinned by tests/golden) "
+                      f"Homing dandelion isaac profile, {E} envs x 20 e-pucks x {steps} env.steps "
+                      f"({el:.1f} s, 1 thread, host CPU)"}
+
+
+def load_traffic(envs: int, sub: int) -> float | None:
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if it matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("envs") != envs or d.get("substeps") != sub:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    E, dp = args.envs, args.decision_period
+    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, rank * E, args.seed, dev)
+    obs, rew, tr = eng.reset()
+    out = (obs, rew, tr)
+
+    n_warm = max(1, math.ceil(args.warmup / dp))
+    n_dec = max(1, args.steps // dp)
+    steps = n_dec * dp
+    # synthetic policy actions for every decision, resident in HBM before timing
+    g = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
+    acts = (torch.randn(n_warm + n_dec, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
+
+    for d in range(n_warm):
+        eng.step(acts[d], dp, out=out)
+    torch.cuda.synchronize(dev)
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_dec)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for d in range(n_dec):
+        ev[d][0].record(stream)
+        eng.step(acts[n_warm + d], dp, out=out)
+        ev[d][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_agent_steps = world * E * N_AGENTS * steps
+    value = total_agent_steps / elapsed
+
+    if rank == 0:
+        bytes_per_launch = ALGO_BYTES_PER_AGENT_STEP * E * N_AGENTS * dp
+        achieved = bytes_per_launch / avg_kernel_s / 1e9
+        traffic = load_traffic(E, dp)
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": n_warm * dp,
+            "ms_per_step": elapsed / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (Homing spawn + in-kernel Philox packet loss; actions N(0,1)->clamp(-3,3)/3 per decision)",
+            "config": {
+                "workload": "SwarmACB-Homing-v0 dandelion, Isaac-profile env.step, 20 e-pucks x "
+                            f"{E} envs per GPU, decision period {dp} fused per launch",
+                "num_envs_per_gpu": E,
+                "num_agents": N_AGENTS,
+                "global_envs": world * E,
+                "decision_period": dp,
+                "parallelism": f"env-sharded x{world}",
+                "agent_decisions_per_s": value / dp,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "step_kernel<HOMING,ISAAC,continuous>",
+                "kernel_avg_us": avg_kernel_s * 1e6,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": cpu_baseline(args.cpu_seconds if world == 1 else 0.0, E),
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+"""ctypes binding of libswarmstep.so (the C ABI declared in include/swarmstep.h).
+
+The product path has no fallback: if the HIP library is missing or fails to
+load, importing the engine raises immediately.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SWARMSTEP_LIB", os.path.join(HERE, "libswarmstep.so"))
+
+ABI_VERSION = 1
+MAX_AGENTS = 64
+MAX_SUBSTEPS = 64
+
+MISSIONS = {"dgt": 0, "xor": 1, "homing": 2, "foraging": 3, "sheltering": 4}
+PROFILES = {"isaac": 0, "standalone": 1}
+
+
+class SwarmParams(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("mission", C.c_int32), ("profile", C.c_int32),
+        ("num_envs", C.c_int32), ("num_agents", C.c_int32), ("obs_dim", C.c_int32),
+        ("discrete_actions", C.c_int32), ("max_episode_length", C.c_int32), ("decimation", C.c_int32),
+        ("reserved0", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
+    ]
+
+
+class SwarmState(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in (
+        "pos_x", "pos_y", "yaw", "fsm", "wheel_l", "wheel_r", "sensor_cache", "ground_prev", "flags",
+        "episode_length", "episode_reward", "completed_reward", "terminal_critic")]
+
+
+class SwarmOutputs(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("reward", C.c_void_p), ("truncated", C.c_void_p)]
+
+
+class SwarmReplay(C.Structure):
+    _fields_ = [
+        ("rab_uniform", C.c_void_p), ("rab_uniform_dispatch", C.c_void_p), ("turn_steps", C.c_void_p),
+        ("spawn_uniform", C.c_void_p), ("spawn_draws", C.c_int32), ("reserved0", C.c_int32),
+        ("spawn_yaw_uniform", C.c_void_p),
+    ]
+
+
+# Every symbol include/swarmstep.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = [
+    "swarm_abi_version", "swarm_strerror", "swarm_last_hip_error", "swarm_create", "swarm_destroy",
+    "swarm_reset", "swarm_step", "swarm_critic_state", "swarm_sync_episode_lengths", "swarm_tick",
+    "swarm_fsm_pack",
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libswarmstep.so (raises if the HIP extension has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libswarmstep.so not found at {LIB_PATH}; build it with "
+            "`make -C swarmacb-isaaclab_amd/csrc` or __graft_entry__.build()")
+    lib = C.CDLL(LIB_PATH)
+    lib.swarm_abi_version.restype = C.c_int32
+    lib.swarm_strerror.restype = C.c_char_p
+    lib.swarm_strerror.argtypes = [C.c_int32]
+    lib.swarm_last_hip_error.restype = C.c_int32
+    lib.swarm_create.restype = C.c_int32
+    lib.swarm_create.argtypes = [C.POINTER(SwarmParams), C.POINTER(C.c_void_p)]
+    lib.swarm_destroy.restype = C.c_int32
+    lib.swarm_destroy.argtypes = [C.c_void_p]
+    lib.swarm_reset.restype = C.c_int32
+    lib.swarm_reset.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_void_p, C.POINTER(SwarmOutputs),
+                                C.POINTER(SwarmReplay), C.c_void_p]
+    lib.swarm_step.restype = C.c_int32
+    lib.swarm_step.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_void_p, C.c_void_p,
+                               C.POINTER(SwarmOutputs), C.c_int32, C.POINTER(SwarmReplay), C.c_void_p]
+    lib.swarm_critic_state.restype = C.c_int32
+    lib.swarm_critic_state.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_void_p, C.c_void_p]
+    lib.swarm_sync_episode_lengths.restype = C.c_int32
+    lib.swarm_sync_episode_lengths.argtypes = [C.c_void_p, C.c_void_p]
+    lib.swarm_tick.restype = C.c_int64
+    lib.swarm_tick.argtypes = [C.c_void_p]
+    lib.swarm_fsm_pack.restype = C.c_uint32
+    lib.swarm_fsm_pack.argtypes = [C.c_int32, C.c_int32, C.c_float] * 3
+    if lib.swarm_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        lib = load()
+        msg = lib.swarm_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: {msg} (status {rc}, hip error {lib.swarm_last_hip_error()})")

@@ -1,0 +1,1122 @@
+// swarm_kernels.hip — fused e-puck env step for CDNA4 (gfx950).
+//
+// One 64-lane wave per workgroup holds floor(64/N) complete arenas (3 for the
+// reference's N = 20 robots: lanes 0-19, 20-39, 40-59), one robot per lane.
+// Everything a robot needs from its arena-mates (positions, "inside" flags)
+// is exchanged through a 64-entry LDS tile; per-arena integer reductions
+// (goal / target / shelter / nest counts, K+ and K-) are wave ballots masked
+// to the arena's lane range + popcount. State lives in registers for all
+// substeps of a launch (the ML-Agents decision period), so HBM sees each state
+// word once per launch, the action once, and the observation once per substep.
+//
+// Reference semantics (file:line of /root/reference):
+//   integrate        epuck_sensors.py:592-617, directional_gate_env.py:816-826 / manual_control.py:355-366
+//   contacts         directional_gate_env.py:658-705, 874-1112 / manual_control.py:467-571
+//   sensors          epuck_sensors.py:85-501 (proximity, light, range-and-bearing)
+//   behaviour        behavior_modules.py:50-574
+//   rewards/dones    directional_gate_env.py:1154-1209, homing_env.py:87-92, xor_aggregation_env.py:126-131,
+//                    foraging_env.py:127-138, sheltering_env.py:157-160 / manual_control.py:372-423
+//   reset            directional_gate_env.py:1215-1273, foraging_env.py:140-151 / manual_control.py:245-269
+//   observation      directional_gate_env.py:1118-1148, epuck_sensors.py:507-539
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swarm_geom.h"
+#include "swarm_launch.h"
+
+namespace swarm {
+
+// ---------------------------------------------------------------------------
+//  Philox4x32-10 (counter-based: results depend only on (seed, counter), so
+//  they are identical however the envs are sharded over GPUs or blocks).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ uint4 rng4(const Geom& g, uint32_t genv, uint32_t robot, uint32_t block,
+                                      uint32_t purpose, uint64_t tick) {
+    uint4 c = make_uint4(genv, robot | (block << 8) | (purpose << 24), (uint32_t)tick, (uint32_t)(tick >> 32));
+    return philox4x32(c, g.seed_lo, g.seed_hi);
+}
+
+// torch-style float uniform from 24 random bits: [0, 1)
+__device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+__device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+// ---------------------------------------------------------------------------
+//  Behaviour FSM packing (layout documented in swarm_capi.cpp swarm_fsm_pack)
+// ---------------------------------------------------------------------------
+struct Fsm {
+    int st, steps;
+    float dir;
+};
+__device__ __forceinline__ int sext(uint32_t v, int bits) { return (int)(v << (32 - bits)) >> (32 - bits); }
+__device__ __forceinline__ Fsm fsm_get(uint32_t f, int sh) {
+    Fsm m;
+    m.st = (f >> sh) & 1u;
+    m.steps = sext((f >> (sh + 1)) & 15u, 4);
+    m.dir = (float)sext((f >> (sh + 5)) & 3u, 2);
+    return m;
+}
+__device__ __forceinline__ uint32_t fsm_put(Fsm m, int sh) {
+    const uint32_t d = (uint32_t)((int)m.dir) & 3u;
+    return (((uint32_t)m.st & 1u) | (((uint32_t)m.steps & 15u) << 1) | (d << 5)) << sh;
+}
+
+// ---------------------------------------------------------------------------
+//  Per-lane context
+// ---------------------------------------------------------------------------
+struct Lane {
+    int lane, a, i, env, ab;  // ab = LDS base of this lane's arena
+    bool valid;
+    uint32_t genv;
+    unsigned long long amask;  // ballot bits of this lane's arena
+};
+
+struct Tile {                 // LDS arena tiles of one wave
+    float x[64];
+    float y[64];
+    int ins[64];
+};
+
+__device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    return __popcll(m & L.amask);
+}
+
+// ---------------------------------------------------------------------------
+//  Collisions
+// ---------------------------------------------------------------------------
+
+// DG:1048-1078 — inward push summed over all penetrated faces (Jacobi).
+__device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
+    float tx = 0.0f, ty = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
+        const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
+        tx += pen * g.face_nx[k];
+        ty += pen * g.face_ny[k];
+    }
+    x = x + tx;
+    y = y + ty;
+}
+
+// MC:531-553 — sequential per face with the robot radius as clearance.
+__device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float sd = (x - g.mcf_px[k]) * g.mcf_nx[k] + (y - g.mcf_py[k]) * g.mcf_ny[k];
+        const float pen = g.wall_clear_mc - sd;
+        if (pen > 0.0f) {
+            x += pen * g.mcf_nx[k];
+            y += pen * g.mcf_ny[k];
+        }
+    }
+}
+
+// DG:1080-1112 / MC:555-571 — Jacobi half-overlap push over pairs i<j.
+__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Tile& T, float& x, float& y) {
+    T.x[L.lane] = x;
+    T.y[L.lane] = y;
+    __syncthreads();
+    // candidate pairs (cheap pass), then the exact terms only for overlapping pairs
+    unsigned long long cand = 0;
+    for (int j = 0; j < g.N; ++j) {
+        const float dx = x - T.x[L.ab + j], dy = y - T.y[L.ab + j];
+        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        if (j != L.i && g.min_dist - dist > 0.0f) cand |= 1ull << j;
+    }
+    const bool any = __any(cand != 0ull);
+    float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
+    if (any) {
+        while (cand) {
+            const int j = __builtin_ctzll(cand);
+            cand &= cand - 1ull;
+            const float dx = x - T.x[L.ab + j], dy = y - T.y[L.ab + j];
+            const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+            const float ov = g.min_dist - dist;
+            const float nx = dx / (dist + 1e-8f), ny = dy / (dist + 1e-8f);
+            if (j > L.i) {  // row term of pair (i, j)
+                rx += ov * nx * 0.5f;
+                ry += ov * ny * 0.5f;
+            } else {        // column term of pair (j, i): n_ji = -n_ij
+                cx += ov * (-nx) * 0.5f;
+                cy += ov * (-ny) * 0.5f;
+            }
+        }
+    }
+    __syncthreads();
+    if (any) {
+        x = (x + rx) - cx;
+        y = (y + ry) - cy;
+    }
+}
+
+// DG:658-705 (DirGate and XOR, which keeps the base-class version)
+__device__ __forceinline__ void gate_dg(const Geom& g, float& x, float& y) {
+    const bool in_y = (y > g.gate_y0) && (y < g.gate_y1);
+    {
+        const float dxl = x - g.gate_hw_neg;
+        if (g.r_robot - fabsf(dxl) > 0.0f && in_y && x < 0.0f) {
+            float s = sgnf(dxl);
+            if (s == 0.0f) s = -1.0f;
+            x = g.gate_hw_neg + s * g.r_robot;
+        }
+    }
+    {
+        const float dxr = x - g.gate_hw_pos;
+        if (g.r_robot - fabsf(dxr) > 0.0f && in_y && x > 0.0f) {
+            float s = sgnf(dxr);
+            if (s == 0.0f) s = 1.0f;
+            x = g.gate_hw_pos + s * g.r_robot;
+        }
+    }
+}
+
+// SH:124-155 / MC:471-496
+__device__ __forceinline__ void gate_shelter(const Geom& g, float& x, float& y) {
+    const bool vy = (y > g.sh_bmr) && (y < g.sh_tpr);
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+        const float x0 = w ? g.sh_r : g.sh_l;
+        const float dx = x - x0;
+        if (fabsf(dx) < g.sh_half && vy) {
+            float s = sgnf(dx);
+            if (s == 0.0f) s = 1.0f;
+            x = x0 + s * g.sh_half;
+        }
+    }
+    const bool hx = (x > g.sh_lmr) && (x < g.sh_rpr);
+    const float dy = y - g.sh_t;
+    if (fabsf(dy) < g.sh_half && hx) {
+        float s = sgnf(dy);
+        if (s == 0.0f) s = 1.0f;
+        y = g.sh_t + s * g.sh_half;
+    }
+}
+
+template <int MISSION, int PROFILE>
+__device__ __forceinline__ void gate_walls(const Geom& g, float& x, float& y) {
+    if constexpr (PROFILE == ISAAC) {
+        // homing_env.py:32-33 and foraging_env.py:42-43 override it to a no-op;
+        // xor_aggregation_env.py does not, so XOR keeps DG's invisible side walls.
+        if constexpr (MISSION == DIRGATE || MISSION == XOR) gate_dg(g, x, y);
+        if constexpr (MISSION == SHELTERING) gate_shelter(g, x, y);
+    } else {
+        if constexpr (MISSION == DIRGATE) gate_dg(g, x, y);          // MC:469-470
+        if constexpr (MISSION == SHELTERING) gate_shelter(g, x, y);
+    }
+}
+
+// DG:898-974 — swept anti-tunnelling against the internal wall segments.
+__device__ __forceinline__ void anti_tunnel(const Geom& g, float& x, float& y, float qx, float qy) {
+    for (int k = 0; k < g.nint; ++k) {
+        const float nx = g.iw_nx[k], ny = g.iw_ny[k], ax = g.iw_ax[k], ay = g.iw_ay[k];
+        const float ps = (qx - ax) * nx + (qy - ay) * ny;
+        const float cs = (x - ax) * nx + (y - ay) * ny;
+        const float den = ps - cs;
+        const bool big = fabsf(den) > 1e-8f;
+        const float st = big ? ps / den : 0.0f;
+        const float ix = qx + (x - qx) * st, iy = qy + (y - qy) * st;
+        const float wu = ((ix - ax) * g.iw_tx[k] + (iy - ay) * g.iw_ty[k]) / g.iw_lsq[k];
+        const bool crossed = (ps * cs < 0.0f) && (st >= 0.0f) && (st <= 1.0f) && (wu >= 0.0f) && (wu <= 1.0f);
+        if (crossed) {
+            float side = sgnf(ps);
+            if (side == 0.0f) side = -sgnf(cs);
+            if (side == 0.0f) side = 1.0f;
+            const float corr = side * g.iw_clear_tunnel - cs;
+            x = x + corr * nx;
+            y = y + corr * ny;
+        }
+    }
+}
+
+// DG:976-1046 — internal walls as capsules (has_prev selects the side rule).
+__device__ __forceinline__ void capsules(const Geom& g, float& x, float& y, bool has_prev, float qx, float qy) {
+    for (int k = 0; k < g.nint; ++k) {
+        const float nx = g.iw_nx[k], ny = g.iw_ny[k], ax = g.iw_ax[k], ay = g.iw_ay[k];
+        const float tx = g.iw_tx[k], ty = g.iw_ty[k];
+        const float rx = x - ax, ry = y - ay;
+        const float u = (rx * tx + ry * ty) / g.iw_lsq[k];
+        const float uc = clampf(u, 0.0f, 1.0f);
+        const float dx = x - (ax + uc * tx), dy = y - (ay + uc * ty);
+        const float raw = sqrtf(dx * dx + dy * dy);
+        const float dist = fmaxf(raw, 1e-8f);
+        const float cs = rx * nx + ry * ny;
+        float side;
+        if (has_prev) {
+            side = sgnf((qx - ax) * nx + (qy - ay) * ny);
+            if (side == 0.0f) side = sgnf(cs);
+        } else {
+            side = sgnf(cs);
+        }
+        if (side == 0.0f) side = 1.0f;
+        const float sdx = side * nx, sdy = side * ny;
+        const bool on_span = (u >= 0.0f) && (u <= 1.0f);
+        const float pdx = on_span ? sdx : (raw > 1e-8f ? dx / dist : sdx);
+        const float pdy = on_span ? sdy : (raw > 1e-8f ? dy / dist : sdy);
+        const float pen = g.iw_clear_capsule - dist;
+        if (pen > 0.0f) {
+            x = x + pen * pdx;
+            y = y + pen * pdy;
+        }
+    }
+}
+
+// DG:874-896 — pre pass, solver iterations, post pass.
+template <int MISSION>
+__device__ __forceinline__ void resolve_collisions(const Geom& g, const Lane& L, Tile& T, float& x, float& y,
+                                                   bool has_prev, float qx, float qy) {
+    constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
+    walls_dg(g, x, y);
+    if constexpr (INTERNAL) {
+        if (has_prev) anti_tunnel(g, x, y, qx, qy);
+        capsules(g, x, y, has_prev, qx, qy);
+    }
+    gate_walls<MISSION, ISAAC>(g, x, y);
+    for (int it = 0; it < 4; ++it) {                     // collision_solver_iterations (DGC:127)
+        const float bx = x, by = y;
+        robots_push(g, L, T, x, y);
+        walls_dg(g, x, y);
+        if constexpr (INTERNAL) {
+            anti_tunnel(g, x, y, bx, by);
+            capsules(g, x, y, true, bx, by);
+        }
+        gate_walls<MISSION, ISAAC>(g, x, y);
+    }
+    walls_dg(g, x, y);
+    if constexpr (INTERNAL) {
+        if (has_prev) anti_tunnel(g, x, y, qx, qy);
+        capsules(g, x, y, has_prev, qx, qy);
+    }
+    gate_walls<MISSION, ISAAC>(g, x, y);
+}
+
+// ---------------------------------------------------------------------------
+//  Ground colour: code 0 black, 1 grey, 2 white (value = 0.5 * code)
+// ---------------------------------------------------------------------------
+template <int MISSION, int PROFILE>
+__device__ __forceinline__ int ground_code(const Geom& g, float x, float y) {
+    int c = 1;
+    if constexpr (MISSION == HOMING) {
+        const float dx = x - g.goal_x, dy = y - g.goal_y;
+        if (dx * dx + dy * dy <= g.disc_r2) c = 0;
+    } else if constexpr (MISSION == XOR || MISSION == SHELTERING) {
+        const float dy = y - 0.0f;
+        const float d0 = x - g.disc_x0, d1 = x - g.disc_x1;
+        if (d0 * d0 + dy * dy <= g.disc_r2 || d1 * d1 + dy * dy <= g.disc_r2) c = 0;
+        if constexpr (MISSION == SHELTERING) {
+            if (x >= g.sh_l && x <= g.sh_r && y >= g.sh_b && y <= g.sh_t) c = 2;
+        }
+    } else if constexpr (MISSION == FORAGING) {
+        const float dy = y - 0.0f;
+        const float d0 = x - g.disc_x0, d1 = x - g.disc_x1;
+        if (d0 * d0 + dy * dy <= g.food_r2 || d1 * d1 + dy * dy <= g.food_r2) c = 0;
+        if (y <= g.z_nest_top) c = 2;
+    } else {  // DIRGATE
+        if (fabsf(x) < g.z_gate_hw && y > g.z_gate_south && y < g.z_corr_south) c = 2;
+        if (fabsf(x) < g.z_corr_hw && y >= g.z_corr_south && y < g.z_ni) c = 0;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+//  Sensors
+// ---------------------------------------------------------------------------
+struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
+    float pv, pa, lv, la, ax, ay;
+};
+
+// ES:85-142, 184-293 : writes the 8 readings to prox[] and the aggregate.
+__device__ __forceinline__ void proximity(const Geom& g, const Lane& L, const Tile& T, float x, float y, float cyw,
+                                          float syw, float prox[8], float& pv, float& pa) {
+    float rdx[8], rdy[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
+        rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
+        prox[k] = 0.0f;
+    }
+    // wall segments: only those whose line passes within the 0.1 m ray length
+    for (int s = 0; s < g.nseg; ++s) {
+        bool near;
+        if (s < 12) {
+            const float sd = (x - g.face_px[s]) * g.face_nx[s] + (y - g.face_py[s]) * g.face_ny[s];
+            near = sd < g.prox_range + 1e-3f;
+        } else {
+            const int k = s - 12;
+            const float rx = x - g.iw_ax[k], ry = y - g.iw_ay[k];
+            const float u = clampf((rx * g.iw_tx[k] + ry * g.iw_ty[k]) / g.iw_lsq[k], 0.0f, 1.0f);
+            const float dx = x - (g.iw_ax[k] + u * g.iw_tx[k]), dy = y - (g.iw_ay[k] + u * g.iw_ty[k]);
+            near = dx * dx + dy * dy < (g.prox_range + 1e-3f) * (g.prox_range + 1e-3f);
+        }
+        if (!near) continue;
+        const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
+        const float qx = ax - x, qy = ay - y;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float den = rdx[k] * sy - rdy[k] * sx;
+            const bool valid = fabsf(den) > 1e-8f;
+            const float dd = den + 1e-12f;
+            const float t = (qx * sy - qy * sx) / dd;
+            const float u = (qx * rdy[k] - qy * rdx[k]) / dd;
+            const bool hit = valid && t >= 0.0f && t <= g.prox_range && u >= 0.0f && u <= 1.0f;
+            const float nr = hit ? 1.0f - t / g.prox_range : 0.0f;
+            prox[k] = fmaxf(prox[k], nr);
+        }
+    }
+    // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
+    unsigned long long cand = 0;
+    for (int j = 0; j < g.N; ++j) {
+        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        if (j != L.i && dx * dx + dy * dy <= 0.0200f) cand |= 1ull << j;
+    }
+    while (cand) {
+        const int j = __builtin_ctzll(cand);
+        cand &= cand - 1ull;
+        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        const float dsq = dx * dx + dy * dy;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float proj = rdx[k] * dx + rdy[k] * dy;
+            const float csq = dsq - proj * proj;
+            const float hc = sqrtf(fmaxf(g.r2 - csq, 0.0f));
+            const float hd = fmaxf(proj - hc, 0.0f);
+            const bool hit = proj > 0.0f && csq <= g.r2 && hd <= g.prox_range;
+            const float rv = clampf(1.0f - hd / g.prox_range, 0.0f, 1.0f);
+            prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
+        }
+    }
+    float sx = 0.0f, sy = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        sx += prox[k] * g.cos_a[k];
+        sy += prox[k] * g.sin_a[k];
+    }
+    pv = fminf(sqrtf(sx * sx + sy * sy), 1.0f);
+    pa = atan2f(sy, sx);
+}
+
+// ES:299-356
+__device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw, float syw, float lt[8], float& lv,
+                                      float& la) {
+    if (!g.has_light) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) lt[k] = 0.0f;
+        lv = 0.0f;
+        la = 0.0f;
+        return;
+    }
+    const float lx = g.light_x - x, ly = g.light_y - y;
+    const float dist = sqrtf(lx * lx + ly * ly + 1e-6f);
+    const float base = g.light_int / (dist / g.unity);
+    const float nlx = lx / (dist + 1e-8f), nly = ly / (dist + 1e-8f);
+    float mx = 0.0f, sx = 0.0f, sy = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float wdx = g.cos_a[k] * cyw - g.sin_a[k] * syw;
+        const float wdy = g.cos_a[k] * syw + g.sin_a[k] * cyw;
+        const float raw = base * fmaxf(wdx * nlx + wdy * nly, 0.0f);
+        lt[k] = clampf(raw, 0.0f, 1.0f);
+        mx = k == 0 ? raw : fmaxf(mx, raw);
+        sx += raw * g.cos_a[k];
+        sy += raw * g.sin_a[k];
+    }
+    const float ang = atan2f(sy, sx);
+    const bool above = mx > g.light_thr;
+    lv = above ? mx : 0.0f;
+    la = above ? ang : 0.0f;
+}
+
+// ES:382-501 — range-and-bearing with line of sight and packet loss.
+// u_replay: this robot's row of N uniforms, or nullptr (Philox stream `purpose`).
+__device__ __forceinline__ void rab(const Geom& g, const Lane& L, const Tile& T, float x, float y, float cyw, float syw,
+                                    const float* u_replay, uint32_t purpose, uint64_t tick, float& zt, float r4[4],
+                                    float& ax_out, float& ay_out) {
+    unsigned long long cand = 0;
+    for (int j = 0; j < g.N; ++j) {
+        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        if (j != L.i && dist < g.rab_range) cand |= 1ull << j;
+    }
+    const bool me_in = T.ins[L.lane] != 0;
+    float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
+    int blk = -1;
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    while (cand) {
+        const int j = __builtin_ctzll(cand);
+        cand &= cand - 1ull;
+        float uu;
+        if (u_replay) {
+            uu = u_replay[j];
+        } else {
+            if ((j >> 2) != blk) {
+                blk = j >> 2;
+                rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
+            }
+            const uint32_t w = (j & 3) == 0 ? rb.x : ((j & 3) == 1 ? rb.y : ((j & 3) == 2 ? rb.z : rb.w));
+            uu = u01(w);
+        }
+        if (!(uu >= g.rab_loss)) continue;
+        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        // line of sight (ES:462-501): arena faces can only block if an end point is
+        // not strictly inside the convex arena; internal walls are always tested.
+        const bool test_arena = !(me_in && T.ins[L.ab + j] != 0);
+        const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
+        bool blocked = false;
+        for (int s = test_arena ? 0 : 12; s < g.nseg; ++s) {
+            const float sx = g.seg_sx[s], sy = g.seg_sy[s];
+            const float qx = g.seg_ax[s] - x, qy = g.seg_ay[s] - y;
+            const float den = rdx * sy - rdy * sx;
+            const float dd = den + 1e-12f;
+            const float t = (qx * sy - qy * sx) / dd;
+            const float u = (qx * rdy - qy * rdx) / dd;
+            blocked |= fabsf(den) > 1e-8f && t > 1e-5f && t < dist - 1e-5f && u >= 0.0f && u <= 1.0f;
+        }
+        if (blocked) continue;
+        n += 1.0f;
+        const float du = dist / g.unity;
+        const float inv = 1.0f / (du + 1e-8f);
+        const float bx = dx * cyw + dy * syw;
+        const float by = -dx * syw + dy * cyw;
+        const float br = atan2f(by, bx);
+        float sb, cb;
+        sincosf(br, &sb, &cb);
+        wx += inv * cb;
+        wy += inv * sb;
+        const float aw = g.alpha / (1.0f + du);
+        axx += aw * cb;
+        ayy += aw * sb;
+    }
+    zt = 1.0f - 2.0f / (1.0f + expf(n));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r4[k] = wx * g.rab_cos[k] + wy * g.rab_sin[k];
+    ax_out = axx;
+    ay_out = ayy;
+}
+
+// ---------------------------------------------------------------------------
+//  Behaviour modules (BM:50-574)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void wheels_from_vector(const Geom& g, float dx, float dy, float& l, float& r) {
+    const bool nz = fabsf(dx) < 1e-5f && fabsf(dy) < 1e-5f;
+    float ang = atan2f(dy, dx);
+    if (ang < 0.0f) ang = ang + g.two_pi_f;
+    const float ca = cosf(ang);
+    const bool front = ang < g.pi_f;
+    float lv = front ? ca : 1.0f, rv = front ? 1.0f : ca;
+    const float sc = g.max_speed / fmaxf(fmaxf(fabsf(lv), fabsf(rv)), 1e-5f);
+    l = nz ? 0.0f : lv * sc;
+    r = nz ? 0.0f : rv * sc;
+}
+
+struct TurnSrc {
+    const int32_t* replay;  // [3][E][N] slice of this substep, or nullptr
+    size_t slot_stride, q;
+    uint64_t tick;
+};
+
+__device__ __forceinline__ int draw_turn(const Geom& g, const Lane& L, const TurnSrc& ts, int slot) {
+    if (ts.replay) return ts.replay[(size_t)slot * ts.slot_stride + ts.q];
+    const uint4 r = rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_TURN + (uint32_t)slot, ts.tick);
+    return 1 + (int)(r.x & 3u);
+}
+
+__device__ __forceinline__ void dispatch(const Geom& g, const Lane& L, int mod, const Agg& s, float prev_l, float prev_r,
+                                         uint32_t& fsm, const TurnSrc& ts, float& l, float& r) {
+    const float ms = g.max_speed;
+    const bool front = s.pv >= g.prox_thr && fabsf(s.pa) <= g.half_pi_f;   // BM:245-251
+    const float tdir = s.pa < 0.0f ? -1.0f : 1.0f;                         // BM:253-264
+    l = 0.0f;
+    r = 0.0f;
+    if (mod == 1) {                                                         // BM:266-341
+        Fsm m = fsm_get(fsm, 0);
+        const bool walking = m.st == 0, was = m.st == 1;
+        if (walking && front) {
+            m.dir = tdir;
+            m.steps = draw_turn(g, L, ts, 0);
+            m.st = 1;
+        }
+        if (was) m.steps -= 1;
+        if (was && m.steps <= 0) m.st = 0;
+        l = was ? m.dir * ms : ms;
+        r = was ? (-m.dir) * ms : ms;
+        fsm = (fsm & ~0xFFu) | fsm_put(m, 0);
+    } else if (mod == 4 || mod == 5) {                                      // BM:343-516
+        const int sh = mod == 4 ? 8 : 16;
+        Fsm m = fsm_get(fsm, sh);
+        const bool was = m.st != 0;
+        if (was) m.steps -= 1;
+        if (was && m.steps <= 0) m.st = 0;
+        const bool trig = !was && m.st == 0 && front;
+        if (trig) {
+            m.dir = tdir;
+            m.steps = draw_turn(g, L, ts, mod - 3);
+            m.st = 1;
+        }
+        fsm = (fsm & ~(0xFFu << sh)) | fsm_put(m, sh);
+        float sla, cla, spa, cpa;
+        sincosf(s.la, &sla, &cla);
+        sincosf(s.pa, &spa, &cpa);
+        const float lx = s.lv * cla, ly = s.lv * sla;
+        const float px = s.pv * cpa, py = s.pv * spa;
+        float vx = mod == 4 ? lx - 0.5f * px : (-lx) - 0.5f * px;
+        float vy = mod == 4 ? ly - 0.5f * py : (-ly) - 0.5f * py;
+        if (sqrtf(vx * vx + vy * vy) < 0.1f) {
+            vx = 1.0f;
+            vy = 0.0f;
+        }
+        float sl, sr;
+        wheels_from_vector(g, vx, vy, sl, sr);
+        l = was ? m.dir * ms : sl;
+        r = was ? (-m.dir) * ms : sr;
+        if (trig) {
+            l = prev_l;
+            r = prev_r;
+        }
+    } else if (mod == 2 || mod == 3) {                                      // BM:518-574
+        float spa, cpa;
+        sincosf(s.pa, &spa, &cpa);
+        const float px = s.pv * cpa, py = s.pv * spa;
+        float vx = mod == 2 ? s.ax - 0.6f * px : (-g.alpha) * s.ax - 0.5f * px;
+        float vy = mod == 2 ? s.ay - 0.6f * py : (-g.alpha) * s.ay - 0.5f * py;
+        if (sqrtf(vx * vx + vy * vy) < 0.1f) {
+            vx = 1.0f;
+            vy = 0.0f;
+        }
+        wheels_from_vector(g, vx, vy, l, r);
+    }
+}
+
+// ---------------------------------------------------------------------------
+//  Critic state (ES:545-586 with DG's centre (0,0), radius 1.2, reference +Y)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void critic5(const Geom& g, float x, float y, float yaw, float* o) {
+    const float nrm = fmaxf(sqrtf(x * x + y * y), 1e-6f);
+    const float hx = x / nrm, hy = y / nrm;
+    float sy, cy;
+    sincosf(yaw, &sy, &cy);
+    o[0] = clampf(nrm / g.critic_radius, 0.0f, 1.0f);
+    o[1] = hx * 0.0f + hy * 1.0f;
+    o[2] = hx * 1.0f - hy * 0.0f;
+    o[3] = cy * hx + sy * hy;
+    o[4] = hx * sy - hy * cy;
+}
+
+// ---------------------------------------------------------------------------
+//  Observation pass (writes obs + returns the aggregates for the cache)
+// ---------------------------------------------------------------------------
+template <int MISSION, int PROFILE>
+__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Tile& T, float x, float y, float yaw,
+                                        const float* u_replay, uint64_t tick, float* obs, Agg& agg) {
+    // publish positions and the strictly-inside flag used by the LOS shortcut
+    bool ins = true;
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+        ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
+    T.x[L.lane] = x;
+    T.y[L.lane] = y;
+    T.ins[L.lane] = ins ? 1 : 0;
+    __syncthreads();
+    float syw, cyw;
+    sincosf(yaw, &syw, &cyw);
+    float prox[8], lt[8], r4[4], zt;
+    proximity(g, L, T, x, y, cyw, syw, prox, agg.pv, agg.pa);
+    light(g, x, y, cyw, syw, lt, agg.lv, agg.la);
+    rab(g, L, T, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, zt, r4, agg.ax, agg.ay);
+    __syncthreads();
+    if (L.valid && obs) {
+        const float gv = 0.5f * (float)ground_code<MISSION, PROFILE>(g, x, y);
+        float* o = obs + ((size_t)L.env * g.N + L.i) * g.obs_dim;
+        if (g.obs_dim == 24) {
+            float4* o4 = reinterpret_cast<float4*>(o);
+            o4[0] = make_float4(prox[0], prox[1], prox[2], prox[3]);
+            o4[1] = make_float4(prox[4], prox[5], prox[6], prox[7]);
+            o4[2] = make_float4(lt[0], lt[1], lt[2], lt[3]);
+            o4[3] = make_float4(lt[4], lt[5], lt[6], lt[7]);
+            o4[4] = make_float4(gv, gv, gv, zt);
+            o4[5] = make_float4(r4[0], r4[1], r4[2], r4[3]);
+        } else {
+            *reinterpret_cast<float4*>(o) = make_float4(gv, gv, gv, zt);
+        }
+    }
+}
+
+// standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
+// proximity/light aggregates equal those of the previous observation (same pose).
+__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Tile& T, float x, float y, float yaw,
+                                         const float* u_replay, uint64_t tick, float& ax, float& ay) {
+    bool ins = true;
+#pragma unroll
+    for (int k = 0; k < 12; ++k)
+        ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
+    T.x[L.lane] = x;
+    T.y[L.lane] = y;
+    T.ins[L.lane] = ins ? 1 : 0;
+    __syncthreads();
+    float syw, cyw, zt, r4[4];
+    sincosf(yaw, &syw, &cyw);
+    rab(g, L, T, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, zt, r4, ax, ay);
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+//  Reset helpers
+// ---------------------------------------------------------------------------
+
+// DG:1215-1240 (+ 1260) spawn rectangle with circle rejection, random yaw.
+__device__ __forceinline__ void spawn_isaac(const Geom& g, const Lane& L, const DevReplay& rp, uint64_t tick, float& x,
+                                            float& y, float& yaw) {
+    const bool rej = g.sp_rad > 0.0f;
+    const int K = rp.spawn ? rp.spawn_k : (rej ? g.sp_attempts + 1 : 1);
+    const size_t q = (size_t)L.env * g.N + L.i;
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < K; ++k) {
+        if (k > 0) {
+            const float rx = x - g.sp_cx, ry = y - g.sp_cy;
+            if (!(sqrtf(rx * rx + ry * ry) > g.sp_rad)) break;
+        }
+        float u0, u1;
+        if (rp.spawn) {
+            const float* p = rp.spawn + (((size_t)k * g.E) * g.N + q) * 2;
+            u0 = p[0];
+            u1 = p[1];
+        } else {
+            if ((k & 1) == 0) rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)(k >> 1), RNG_SPAWN, tick);
+            u0 = u01((k & 1) ? rb.z : rb.x);
+            u1 = u01((k & 1) ? rb.w : rb.y);
+        }
+        x = g.sp_cx + (u0 - 0.5f) * g.sp_sx;
+        y = g.sp_cy + (u1 - 0.5f) * g.sp_sy;
+        if (!rej) break;
+    }
+    const float uy = rp.spawn_yaw ? rp.spawn_yaw[q]
+                                  : u01(rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_SPAWN_YAW, tick).x);
+    yaw = uy * 2.0f * g.pi_f - g.pi_f;
+}
+
+// MC:250-258 polar spawn in the safe disc; homing keeps the northern half.
+template <int MISSION>
+__device__ __forceinline__ void spawn_mc(const Geom& g, const Lane& L, const DevReplay& rp, uint64_t tick, float& x,
+                                         float& y, float& yaw) {
+    float ur, ut, uy;
+    const size_t q = (size_t)L.env * g.N + L.i;
+    if (rp.spawn) {
+        const size_t EN = (size_t)g.E * g.N;
+        ur = rp.spawn[q];
+        ut = rp.spawn[EN + q];
+        uy = rp.spawn[2 * EN + q];
+    } else {
+        const uint4 r = rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_SPAWN, tick);
+        ur = u01(r.x);
+        ut = u01(r.y);
+        uy = u01(r.z);
+    }
+    const float rr = sqrtf(ur) * g.mc_safe;
+    const float th = ut * g.mc_th_scale;
+    x = rr * cosf(th);
+    y = rr * sinf(th);
+    if constexpr (MISSION == HOMING) y = fabsf(y);
+    yaw = uy * 2.0f * g.pi_f - g.pi_f;
+}
+
+// ---------------------------------------------------------------------------
+//  Rewards (returns the team reward of this lane's arena)
+// ---------------------------------------------------------------------------
+template <int MISSION, int PROFILE>
+__device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float x, float y, int& gprev, int& flags,
+                                             bool is_final) {
+    if constexpr (MISSION == HOMING) {
+        const float dx = x - g.goal_x, dy = y - g.goal_y;
+        const int cnt = arena_count(L, L.valid && dx * dx + dy * dy <= g.disc_r2);
+        return is_final ? (float)cnt : 0.0f;
+    } else if constexpr (MISSION == XOR) {
+        const float dy = y - 0.0f, d0 = x - g.disc_x0, d1 = x - g.disc_x1;
+        const int c0 = arena_count(L, L.valid && d0 * d0 + dy * dy <= g.disc_r2);
+        const int c1 = arena_count(L, L.valid && d1 * d1 + dy * dy <= g.disc_r2);
+        return (float)(c0 > c1 ? c0 : c1);
+    } else if constexpr (MISSION == FORAGING) {
+        bool food;
+        if constexpr (PROFILE == ISAAC) {   // FO:110-114 axis-aligned pickup
+            food = (fabsf(x - g.disc_x0) <= g.food_r && fabsf(y - 0.0f) <= g.food_r) ||
+                   (fabsf(x - g.disc_x1) <= g.food_r && fabsf(y - 0.0f) <= g.food_r);
+        } else {                            // MC:315-317 disc
+            const float dy = y - 0.0f, d0 = x - g.disc_x0, d1 = x - g.disc_x1;
+            food = d0 * d0 + dy * dy <= g.food_r2 || d1 * d1 + dy * dy <= g.food_r2;
+        }
+        const bool nest = y <= g.z_nest_top;
+        const bool hf = (flags & 1) || food;
+        bool arrived = nest && hf;
+        if constexpr (PROFILE == STANDALONE) arrived = arrived && !(flags & 2);   // MC:389
+        const int cnt = arena_count(L, L.valid && arrived);
+        flags = ((arrived ? false : hf) ? 1 : 0) | (nest ? 2 : 0);
+        return (float)cnt;
+    } else if constexpr (MISSION == SHELTERING) {
+        const bool in = x >= g.sh_l && x <= g.sh_r && y >= g.sh_b && y <= g.sh_t;
+        return (float)arena_count(L, L.valid && in);
+    } else {  // DIRGATE colour transitions (DG:1154-1194)
+        const int cur = ground_code<MISSION, PROFILE>(g, x, y);
+        const int kp = arena_count(L, L.valid && gprev == 0 && cur == 2);
+        const int km = arena_count(L, L.valid && gprev == 2 && cur == 0);
+        gprev = cur;
+        return (float)kp - (float)km;
+    }
+}
+
+// ---------------------------------------------------------------------------
+//  The fused step kernel
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ Lane make_lane(const Geom& g) {
+    Lane L;
+    L.lane = threadIdx.x;
+    L.a = L.lane / g.N;
+    L.i = L.lane - L.a * g.N;
+    L.env = blockIdx.x * g.apb + L.a;
+    L.valid = (L.a < g.apb) && (L.env < g.E);
+    L.ab = (L.a < g.apb ? L.a : 0) * g.N;
+    const uint64_t goff = ((uint64_t)g.env_off_hi << 32) | g.env_off_lo;
+    L.genv = (uint32_t)(goff + (uint64_t)(L.env < g.E ? L.env : 0));
+    const unsigned long long m = g.N >= 64 ? ~0ull : ((1ull << g.N) - 1ull);
+    L.amask = (L.a < g.apb) ? (m << L.ab) : 0ull;
+    return L;
+}
+
+template <int MISSION, int PROFILE, bool DISCRETE>
+__global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
+                                                  const float* __restrict__ ovr, const DevOut out, const DevReplay rp,
+                                                  uint64_t tick0, int n_sub, uint64_t reset_any) {
+    __shared__ Tile T;
+    const Lane L = make_lane(g);
+    const size_t q = L.valid ? (size_t)L.env * g.N + L.i : 0;
+    const size_t EN = (size_t)g.E * g.N;
+
+    // ---- load state (invalid lanes keep harmless values) ----
+    float x = 0.0f, y = 0.0f, yaw = 0.0f, wl = 0.0f, wr = 0.0f;
+    uint32_t fsm = 0;
+    int gprev = 1, flags = 0, ep_len = 0;
+    float ep_rew = 0.0f, comp = 0.0f;
+    Agg cache = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    float ax = 0.0f, ay = 0.0f;
+    int mod = 0;
+    float ox = NAN, oy = NAN;
+    if (L.valid) {
+        x = st.x[q];
+        y = st.y[q];
+        yaw = st.yaw[q];
+        fsm = st.fsm[q];
+        wl = st.wl[q];
+        wr = st.wr[q];
+        gprev = st.gprev[q];
+        flags = st.flags[q];
+        ep_len = st.ep_len[L.env];
+        ep_rew = st.ep_rew[L.env];
+        comp = st.comp_rew[L.env];
+        if constexpr (DISCRETE || PROFILE == STANDALONE) {
+            cache.pv = st.cache[q];
+            cache.pa = st.cache[EN + q];
+            cache.lv = st.cache[2 * EN + q];
+            cache.la = st.cache[3 * EN + q];
+            cache.ax = st.cache[4 * EN + q];
+            cache.ay = st.cache[5 * EN + q];
+        }
+        if constexpr (DISCRETE) {
+            mod = reinterpret_cast<const int32_t*>(actions)[q];
+        } else {
+            const float2 a = reinterpret_cast<const float2*>(actions)[q];
+            ax = a.x;
+            ay = a.y;
+        }
+        if (ovr) {
+            ox = ovr[2 * q];
+            oy = ovr[2 * q + 1];
+        }
+    }
+    float rew_acc = 0.0f;
+    bool trunc_acc = false;
+
+    for (int s = 0; s < n_sub; ++s) {
+        const uint64_t tick = tick0 + (uint64_t)s;
+        const size_t NN = (size_t)g.N * g.N;
+        const float* u_obs = rp.rab ? rp.rab + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * g.N : nullptr;
+        TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, EN, q, tick};
+
+        // ------------------------------ actions ------------------------------
+        float lw, rw;
+        if constexpr (PROFILE == STANDALONE) {
+            const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * g.N
+                                        : nullptr;
+            rab_only(g, L, T, x, y, yaw, u_d, tick, cache.ax, cache.ay);
+            if constexpr (DISCRETE) {
+                dispatch(g, L, mod, cache, 0.0f, 0.0f, fsm, ts, lw, rw);   // previous = zeros (MC:744-747)
+            } else {
+                lw = ax * g.max_speed;
+                rw = ay * g.max_speed;
+            }
+            if (!isnan(ox)) {
+                lw = ox;
+                rw = oy;
+            }
+            lw = clampf(lw, -g.max_speed, g.max_speed);                      // MC:357-358
+            rw = clampf(rw, -g.max_speed, g.max_speed);
+        } else {
+            if constexpr (DISCRETE) {
+                dispatch(g, L, mod, cache, wl, wr, fsm, ts, lw, rw);         // DG:782-795
+            } else {
+                lw = clampf(ax, -1.0f, 1.0f) * g.max_speed;                  // DG:807-809
+                rw = clampf(ay, -1.0f, 1.0f) * g.max_speed;
+            }
+        }
+        wl = lw;
+        wr = rw;
+
+        // ------------------------------ physics ------------------------------
+        const int nd = PROFILE == ISAAC ? g.decimation : 1;
+        for (int d = 0; d < nd; ++d) {
+            const float qx = x, qy = y;
+            const float v = 0.5f * (lw + rw);
+            const float om = (rw - lw) / g.wheelbase;
+            float sy, cy;
+            sincosf(yaw, &sy, &cy);
+            x += v * cy * g.dt;
+            y += v * sy * g.dt;
+            const float yw = yaw + om * g.dt;
+            float syw, cyw;
+            sincosf(yw, &syw, &cyw);
+            yaw = atan2f(syw, cyw);
+            if constexpr (PROFILE == ISAAC) {
+                walls_dg(g, x, y);
+                gate_walls<MISSION, ISAAC>(g, x, y);
+                robots_push(g, L, T, x, y);
+                resolve_collisions<MISSION>(g, L, T, x, y, true, qx, qy);
+            } else {
+                walls_mc(g, x, y);
+                gate_walls<MISSION, STANDALONE>(g, x, y);
+                robots_push(g, L, T, x, y);
+            }
+        }
+
+        // ------------------------- dones / rewards / reset -------------------------
+        bool tout;
+        if constexpr (PROFILE == ISAAC) {
+            ep_len += 1;
+            tout = ep_len >= g.max_len;                                      // DG:1200-1209
+            if (tout && L.valid) {
+                float c5[5];
+                critic5(g, x, y, yaw, c5);
+                float* o = st.tcrit + q * 5;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) o[k] = c5[k];
+            }
+            const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, tout);
+            ep_rew += r;
+            rew_acc += r;
+            if (tout) {                                                      // DG:1242-1273
+                ep_len = 0;
+                comp = ep_rew;
+                ep_rew = 0.0f;
+                if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
+            }
+            if ((reset_any >> s) & 1ull) {                                   // DG:1262 (all envs)
+                resolve_collisions<MISSION>(g, L, T, x, y, false, 0.0f, 0.0f);
+            }
+            if (tout) {
+                gprev = ground_code<MISSION, PROFILE>(g, x, y);
+                fsm = 0u;
+                if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
+            }
+        } else {
+            const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, ep_len + 1 >= g.max_len);
+            ep_rew += r;
+            rew_acc += r;
+            ep_len += 1;
+            tout = ep_len >= g.max_len;                                      // MC:753-754
+            if (tout) {
+                comp = ep_rew;
+                if (L.valid) spawn_mc<MISSION>(g, L, rp, tick, x, y, yaw);
+                gprev = ground_code<MISSION, PROFILE>(g, x, y);
+                flags = (y <= g.z_nest_top) ? 2 : 0;
+                fsm = 0u;
+                ep_rew = 0.0f;
+                ep_len = 0;
+            }
+        }
+        trunc_acc |= tout;
+
+        // ---------------------------- observation ----------------------------
+        observe<MISSION, PROFILE>(g, L, T, x, y, yaw, u_obs, tick, out.obs, cache);
+    }
+
+    // ---- store state and per-call outputs ----
+    if (L.valid) {
+        st.x[q] = x;
+        st.y[q] = y;
+        st.yaw[q] = yaw;
+        st.fsm[q] = fsm;
+        st.wl[q] = wl;
+        st.wr[q] = wr;
+        st.gprev[q] = (uint8_t)gprev;
+        st.flags[q] = (uint8_t)flags;
+        st.cache[q] = cache.pv;
+        st.cache[EN + q] = cache.pa;
+        st.cache[2 * EN + q] = cache.lv;
+        st.cache[3 * EN + q] = cache.la;
+        st.cache[4 * EN + q] = cache.ax;
+        st.cache[5 * EN + q] = cache.ay;
+        if (L.i == 0) {
+            st.ep_len[L.env] = ep_len;
+            st.ep_rew[L.env] = ep_rew;
+            st.comp_rew[L.env] = comp;
+            if (out.reward) out.reward[L.env] = rew_acc;
+            if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+//  Reset kernel: _reset_idx(mask) + observations (DirectMARLEnv.reset)
+// ---------------------------------------------------------------------------
+template <int MISSION, int PROFILE>
+__global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState st, const uint8_t* __restrict__ mask,
+                                                   const DevOut out, const DevReplay rp, uint64_t tick) {
+    __shared__ Tile T;
+    const Lane L = make_lane(g);
+    const size_t q = L.valid ? (size_t)L.env * g.N + L.i : 0;
+    const size_t EN = (size_t)g.E * g.N;
+    float x = 0.0f, y = 0.0f, yaw = 0.0f;
+    bool doit = false;
+    if (L.valid) {
+        x = st.x[q];
+        y = st.y[q];
+        yaw = st.yaw[q];
+        doit = mask == nullptr || mask[L.env] != 0;
+    }
+    if (doit) {
+        if constexpr (PROFILE == ISAAC) {
+            spawn_isaac(g, L, rp, tick, x, y, yaw);
+        } else {
+            spawn_mc<MISSION>(g, L, rp, tick, x, y, yaw);
+        }
+    }
+    if constexpr (PROFILE == ISAAC) {
+        resolve_collisions<MISSION>(g, L, T, x, y, false, 0.0f, 0.0f);      // DG:1262 (all envs)
+    }
+    Agg agg;
+    const float* u_obs = rp.rab ? rp.rab + (size_t)(L.valid ? L.env : 0) * g.N * g.N + (size_t)L.i * g.N : nullptr;
+    observe<MISSION, PROFILE>(g, L, T, x, y, yaw, u_obs, tick, out.obs, agg);
+    if (L.valid) {
+        st.x[q] = x;
+        st.y[q] = y;
+        st.yaw[q] = yaw;
+        st.cache[q] = agg.pv;
+        st.cache[EN + q] = agg.pa;
+        st.cache[2 * EN + q] = agg.lv;
+        st.cache[3 * EN + q] = agg.la;
+        st.cache[4 * EN + q] = agg.ax;
+        st.cache[5 * EN + q] = agg.ay;
+        if (doit) {
+            st.fsm[q] = 0u;
+            st.gprev[q] = (uint8_t)ground_code<MISSION, PROFILE>(g, x, y);
+            // prev_in_nest: FO:151 (isaac foraging only) / MC:267 (standalone, every mission)
+            st.flags[q] = (uint8_t)(((PROFILE == STANDALONE || MISSION == FORAGING) && y <= g.z_nest_top) ? 2 : 0);
+            st.wl[q] = 0.0f;
+            st.wr[q] = 0.0f;
+            if (L.i == 0) {
+                if constexpr (PROFILE == ISAAC) st.comp_rew[L.env] = st.ep_rew[L.env];
+                st.ep_rew[L.env] = 0.0f;
+                st.ep_len[L.env] = 0;
+                if (out.reward) out.reward[L.env] = 0.0f;
+                if (out.trunc) out.trunc[L.env] = 0;
+            }
+        }
+    }
+}
+
+__global__ void critic_kernel(const Geom g, const float* __restrict__ x, const float* __restrict__ y,
+                              const float* __restrict__ yaw, float* __restrict__ out) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (size_t)g.E * g.N) return;
+    critic5(g, x[q], y[q], yaw[q], out + q * 5);
+}
+
+// ---------------------------------------------------------------------------
+//  Host-side launchers (called by swarm_capi.cpp)
+// ---------------------------------------------------------------------------
+template <int M, int P, bool D>
+static void launch_step_t(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
+                          const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
+    const int blocks = (g.E + g.apb - 1) / g.apb;
+    hipLaunchKernelGGL((step_kernel<M, P, D>), dim3(blocks), dim3(64), 0, stream, g, st, act, ovr, out, rp, tick, n_sub,
+                       reset_any);
+}
+
+template <int M, int P>
+static void launch_step_md(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
+                           const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
+    if (g.discrete)
+        launch_step_t<M, P, true>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
+    else
+        launch_step_t<M, P, false>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
+}
+
+template <int M>
+static void launch_step_m(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
+                          const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
+    if (g.profile == ISAAC)
+        launch_step_md<M, ISAAC>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
+    else
+        launch_step_md<M, STANDALONE>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
+}
+
+void launch_step(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
+                 const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
+    switch (g.mission) {
+    case DIRGATE: launch_step_m<DIRGATE>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
+    case XOR: launch_step_m<XOR>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
+    case HOMING: launch_step_m<HOMING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
+    case FORAGING: launch_step_m<FORAGING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
+    default: launch_step_m<SHELTERING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
+    }
+}
+
+template <int M>
+static void launch_reset_m(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out,
+                           const DevReplay& rp, uint64_t tick, hipStream_t stream) {
+    const int blocks = (g.E + g.apb - 1) / g.apb;
+    if (g.profile == ISAAC)
+        hipLaunchKernelGGL((reset_kernel<M, ISAAC>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp, tick);
+    else
+        hipLaunchKernelGGL((reset_kernel<M, STANDALONE>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp,
+                           tick);
+}
+
+void launch_reset(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out, const DevReplay& rp,
+                  uint64_t tick, hipStream_t stream) {
+    switch (g.mission) {
+    case DIRGATE: launch_reset_m<DIRGATE>(g, st, mask, out, rp, tick, stream); break;
+    case XOR: launch_reset_m<XOR>(g, st, mask, out, rp, tick, stream); break;
+    case HOMING: launch_reset_m<HOMING>(g, st, mask, out, rp, tick, stream); break;
+    case FORAGING: launch_reset_m<FORAGING>(g, st, mask, out, rp, tick, stream); break;
+    default: launch_reset_m<SHELTERING>(g, st, mask, out, rp, tick, stream); break;
+    }
+}
+
+void launch_critic(const Geom& g, const float* x, const float* y, const float* yaw, float* out, hipStream_t stream) {
+    const size_t n = (size_t)g.E * g.N;
+    const int blocks = (int)((n + 255) / 256);
+    hipLaunchKernelGGL(critic_kernel, dim3(blocks), dim3(256), 0, stream, g, x, y, yaw, out);
+}
+
+}  // namespace swarm

@@ -1,0 +1,88 @@
+"""libswarmstep.so loads, exports every symbol include/swarmstep.h declares, and its
+host-only entry points (validation, FSM packing, episode mirror) behave — no GPU needed."""
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from SwarmACB_isaac import _native
+from SwarmACB_isaac.engine import fsm_pack, fsm_unpack
+
+HEADER = os.path.join(ROOT, "include", "swarmstep.h")
+
+
+def declared_functions() -> list[str]:
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(swarm_[a-z_]+)\s*\(", text)))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == sorted(_native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.swarm_abi_version() == _native.ABI_VERSION
+    assert lib.swarm_strerror(0) == b"ok"
+    assert lib.swarm_strerror(-1) == b"invalid argument"
+
+
+def _params(**kw):
+    p = dict(abi_version=1, mission=2, profile=0, num_envs=4, num_agents=20, obs_dim=24, discrete_actions=0,
+             max_episode_length=1200, decimation=1, reserved0=0, env_offset=0, seed=0)
+    p.update(kw)
+    return _native.SwarmParams(**p)
+
+
+@pytest.mark.parametrize("bad", [dict(abi_version=2), dict(mission=9), dict(profile=3), dict(num_envs=0),
+                                 dict(num_agents=65), dict(num_agents=0), dict(obs_dim=7),
+                                 dict(max_episode_length=0), dict(env_offset=-1)])
+def test_create_rejects_bad_params(bad):
+    lib = _native.load()
+    h = C.c_void_p()
+    rc = lib.swarm_create(C.byref(_params(**bad)), C.byref(h))
+    assert rc in (-1, -2) and not h.value
+
+
+def test_create_destroy_and_call_order():
+    lib = _native.load()
+    h = C.c_void_p()
+    assert lib.swarm_create(C.byref(_params()), C.byref(h)) == 0 and h.value
+    assert lib.swarm_tick(h) == 0
+    # step before reset is refused before any device work happens
+    st = _native.SwarmState(*([1] * 13))
+    out = _native.SwarmOutputs(1, 1, 1)
+    assert lib.swarm_step(h, C.byref(st), C.c_void_p(1), None, C.byref(out), 1, None, None) == -4
+    assert lib.swarm_step(h, C.byref(st), C.c_void_p(1), None, C.byref(out), 0, None, None) == -1
+    assert lib.swarm_step(h, C.byref(st), C.c_void_p(1), None, C.byref(out), 65, None, None) == -1
+    lens = np.full(4, 7, np.int32)
+    assert lib.swarm_sync_episode_lengths(h, lens.ctypes.data_as(C.c_void_p)) == 0
+    assert lib.swarm_destroy(h) == 0
+
+
+def test_fsm_pack_matches_c_abi():
+    lib = _native.load()
+    rng = np.random.default_rng(0)
+    f = {
+        "ex_state": rng.integers(0, 2, 500), "ex_steps": rng.integers(-1, 5, 500),
+        "ex_dir": rng.choice([-1.0, 0.0, 1.0], 500),
+        "ph_avoid": rng.integers(0, 2, 500), "ph_steps": rng.integers(-1, 5, 500),
+        "ph_dir": rng.choice([-1.0, 0.0, 1.0], 500),
+        "ap_avoid": rng.integers(0, 2, 500), "ap_steps": rng.integers(-1, 5, 500),
+        "ap_dir": rng.choice([-1.0, 0.0, 1.0], 500),
+    }
+    w = fsm_pack(f)
+    for q in range(0, 500, 37):
+        c = lib.swarm_fsm_pack(*[f[k][q].item() for k in ("ex_state", "ex_steps", "ex_dir", "ph_avoid",
+                                                           "ph_steps", "ph_dir", "ap_avoid", "ap_steps", "ap_dir")])
+        assert c == int(w[q])
+    back = fsm_unpack(w)
+    for k, v in f.items():
+        np.testing.assert_array_equal(back[k], v.astype(back[k].dtype))
