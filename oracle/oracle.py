@@ -169,6 +169,21 @@ class OracleEnv:
         return out
 
 
+class libm_perturb:
+    """Context manager: every oracle cos/sin/atan2/exp result nudged by `ulps` ulp."""
+
+    def __init__(self, ulps: int):
+        self.ulps = int(ulps)
+
+    def __enter__(self):
+        lib().or_set_libm_perturb(self.ulps)
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_libm_perturb(0)
+        return False
+
+
 def seed(s: int):
     lib().or_seed(int(s))
 

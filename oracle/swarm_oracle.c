@@ -154,6 +154,26 @@ static void build_geom(const or_cfg* c, geom* g) {
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/*  libm conditioning probe. The reference evaluates cos/sin/atan2/exp with  */
+/*  torch's CPU kernels (SLEEF), this oracle with glibc and the HIP kernel   */
+/*  with ocml; each is within ~1 ulp of the true value but they differ. The  */
+/*  parity envelope (tests/parity.py) re-runs the oracle with every such     */
+/*  result nudged by +-g_lm_ulps ulp to measure how far a step's outputs can */
+/*  move under that freedom. 0 (the default) = plain libm.                   */
+/* ------------------------------------------------------------------------ */
+static int g_lm_ulps = 0;
+void or_set_libm_perturb(int ulps) { g_lm_ulps = ulps; }
+static inline float lm_nudge(float v) {
+    for (int k = 0; k < g_lm_ulps; k++) v = nextafterf(v, INFINITY);
+    for (int k = 0; k < -g_lm_ulps; k++) v = nextafterf(v, -INFINITY);
+    return v;
+}
+static inline float lm_cos(float a) { return lm_nudge(cosf(a)); }
+static inline float lm_sin(float a) { return lm_nudge(sinf(a)); }
+static inline float lm_atan2(float y, float x) { return lm_nudge(atan2f(y, x)); }
+static inline float lm_exp(float a) { return lm_nudge(expf(a)); }
+
 /* physical constants (DGC:122-137, 179; MC:118-121, 185-189) */
 #define R_ROBOT 0.035
 #define MAX_SPEED 0.16f
@@ -475,7 +495,7 @@ typedef struct {
 static void proximity(const or_cfg* c, const geom* g, const float* pos, const float* yaw, int e, int i, bundle* b) {
     const int N = c->N;
     const float* P = pos + (size_t)e * N * 2;
-    float cy = cosf(yaw[(size_t)e * N + i]), sy = sinf(yaw[(size_t)e * N + i]);
+    float cy = lm_cos(yaw[(size_t)e * N + i]), sy = lm_sin(yaw[(size_t)e * N + i]);
     float ox = P[2 * i], oy = P[2 * i + 1];
     float rdx[8], rdy[8], rd[8];
     for (int k = 0; k < 8; k++) {
@@ -525,7 +545,7 @@ static void proximity(const or_cfg* c, const geom* g, const float* pos, const fl
     }
     float mag = sqrtf(sx * sx + sy3 * sy3);
     b->prox_value = mag > 1.0f ? 1.0f : mag;
-    b->prox_angle = atan2f(sy3, sx);
+    b->prox_angle = lm_atan2(sy3, sx);
 }
 
 /* ES:299-356 */
@@ -542,7 +562,7 @@ static void light(const or_cfg* c, const geom* g, const float* pos, const float*
     float dist = sqrtf(lx * lx + ly * ly + 1e-6f);
     float du = dist / UNITY;
     float base = LIGHT_INT / du;
-    float cy = cosf(yaw[(size_t)e * N + i]), sy = sinf(yaw[(size_t)e * N + i]);
+    float cy = lm_cos(yaw[(size_t)e * N + i]), sy = lm_sin(yaw[(size_t)e * N + i]);
     float nlx = lx / (dist + 1e-8f), nly = ly / (dist + 1e-8f);
     float raw[8], mx = 0.0f, sx = 0.0f, sy2 = 0.0f;
     for (int k = 0; k < 8; k++) {
@@ -556,7 +576,7 @@ static void light(const or_cfg* c, const geom* g, const float* pos, const float*
         sx += raw[k] * g->cos_a[k];
         sy2 += raw[k] * g->sin_a[k];
     }
-    float ang = atan2f(sy2, sx);
+    float ang = lm_atan2(sy2, sx);
     int above = mx > LIGHT_THR;
     b->light_value = above ? mx : 0.0f;
     b->light_angle = above ? ang : 0.0f;
@@ -567,7 +587,7 @@ static void rab(const or_cfg* c, const geom* g, const float* pos, const float* y
                 const float* u, bundle* b) {
     const int N = c->N;
     const float* P = pos + (size_t)e * N * 2;
-    float cy = cosf(yaw[(size_t)e * N + i]), sy = sinf(yaw[(size_t)e * N + i]);
+    float cy = lm_cos(yaw[(size_t)e * N + i]), sy = lm_sin(yaw[(size_t)e * N + i]);
     float ox = P[2 * i], oy = P[2 * i + 1];
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
     for (int j = 0; j < N; j++) {
@@ -594,15 +614,15 @@ static void rab(const or_cfg* c, const geom* g, const float* pos, const float* y
         float inv = 1.0f / (du + 1e-8f);
         float bx = dx * cy + dy * sy;
         float by = -dx * sy + dy * cy;
-        float br = atan2f(by, bx);
-        float cb = cosf(br), sb = sinf(br);
+        float br = lm_atan2(by, bx);
+        float cb = lm_cos(br), sb = lm_sin(br);
         wx += inv * cb * inf;
         wy += inv * sb * inf;
         float aw = ALPHA / (1.0f + du);
         axx += aw * cb * inf;
         ayy += aw * sb * inf;
     }
-    b->ztilde = 1.0f - 2.0f / (1.0f + expf(n));
+    b->ztilde = 1.0f - 2.0f / (1.0f + lm_exp(n));
     for (int k = 0; k < 4; k++) b->rab4[k] = wx * g->rab_cos[k] + wy * g->rab_sin[k];
     b->attr_x = axx;
     b->attr_y = ayy;
@@ -615,9 +635,9 @@ static void rab(const or_cfg* c, const geom* g, const float* pos, const float* y
 /* BM:50-90 */
 static void wheels_from_vector(float dx, float dy, float* l, float* r) {
     int nz = (fabsf(dx) < 1e-5f) && (fabsf(dy) < 1e-5f);
-    float ang = atan2f(dy, dx);
+    float ang = lm_atan2(dy, dx);
     if (ang < 0.0f) ang = ang + (float)(2.0 * PI_D);
-    float ca = cosf(ang);
+    float ca = lm_cos(ang);
     int front = ang < (float)PI_D;
     float lv = front ? ca : 1.0f, rv = front ? 1.0f : ca;
     float mv = fabsf(lv) > fabsf(rv) ? fabsf(lv) : fabsf(rv);
@@ -697,8 +717,8 @@ static void dispatch_one(or_state* st, size_t idx, int e, int i, int mod,
         }
         av[idx] = avoiding; sp[idx] = steps; dr[idx] = dir;
         float lt = dir * ms, rt = (-dir) * ms;
-        float lx = lv_ * cosf(la), ly = lv_ * sinf(la);
-        float px = pv * cosf(pa), py = pv * sinf(pa);
+        float lx = lv_ * lm_cos(la), ly = lv_ * lm_sin(la);
+        float px = pv * lm_cos(pa), py = pv * lm_sin(pa);
         float vx, vy;
         if (mod == 4) { vx = lx - 0.5f * px; vy = ly - 0.5f * py; }
         else { vx = (-lx) - 0.5f * px; vy = (-ly) - 0.5f * py; }
@@ -712,7 +732,7 @@ static void dispatch_one(or_state* st, size_t idx, int e, int i, int mod,
         break;
     }
     case 2: case 3: {                                                   /* BM:518-574 */
-        float px = pv * cosf(pa), py = pv * sinf(pa);
+        float px = pv * lm_cos(pa), py = pv * lm_sin(pa);
         float vx, vy;
         if (mod == 2) { vx = rx_ - 0.6f * px; vy = ry_ - 0.6f * py; }
         else { vx = (-ALPHA) * rx_ - 0.5f * px; vy = (-ALPHA) * ry_ - 0.5f * py; }
@@ -745,7 +765,7 @@ void or_critic_state(const or_cfg* c, const float* pos, const float* yaw, float*
         float hx = rx / nrm, hy = ry / nrm;
         float ca = hx * 0.0f + hy * 1.0f;
         float sa = hx * 1.0f - hy * 0.0f;
-        float cy = cosf(yaw[q]), sy = sinf(yaw[q]);
+        float cy = lm_cos(yaw[q]), sy = lm_sin(yaw[q]);
         float cb = cy * hx + sy * hy;
         float sb = hx * sy - hy * cy;
         float* o = out + q * 5;
@@ -945,12 +965,12 @@ static void drive(const or_cfg* c, or_state* st, int e, const float* L, const fl
         size_t q = (size_t)e * c->N + i;
         float v = 0.5f * (L[i] + R[i]);
         float om = (R[i] - L[i]) / WHEELBASE;
-        float cy = cosf(st->yaw[q]), sy = sinf(st->yaw[q]);
+        float cy = lm_cos(st->yaw[q]), sy = lm_sin(st->yaw[q]);
         float dx = v * cy * DT, dy = v * sy * DT, dyaw = om * DT;
         st->pos[2 * q] += dx;
         st->pos[2 * q + 1] += dy;
         float yw = st->yaw[q] + dyaw;
-        st->yaw[q] = atan2f(sinf(yw), cosf(yw));
+        st->yaw[q] = lm_atan2(lm_sin(yw), lm_cos(yw));
     }
 }
 
@@ -1146,7 +1166,7 @@ static void mc_reset_env(const or_cfg* c, const geom* g, or_state* st, int e, co
         size_t q = (size_t)e * N + i;
         float r = sqrtf(ur[i]) * (float)safe;
         float th = ut[i] * (float)(c->mission == OR_HOMING ? PI_D : 2 * PI_D);
-        float x = r * cosf(th), y = r * sinf(th);
+        float x = r * lm_cos(th), y = r * lm_sin(th);
         if (c->mission == OR_HOMING) y = fabsf(y);
         st->pos[2 * q] = x;
         st->pos[2 * q + 1] = y;

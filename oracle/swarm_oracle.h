@@ -84,6 +84,9 @@ void or_rng_uniform(float* out, int n);
 /* compute_critic_state_5d (ES:545-586) with DG's centre/radius/reference. */
 void or_critic_state(const or_cfg* cfg, const float* pos, const float* yaw, float* out);
 
+/* Nudge every cos/sin/atan2/exp result by `ulps` ulp (0 = off): conditioning probe for tests. */
+void or_set_libm_perturb(int ulps);
+
 /* Seed the oracle's private generator (MT19937, torch-compatible stream). */
 void or_seed(uint64_t seed);
 

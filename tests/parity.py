@@ -5,11 +5,13 @@ Tolerance (stated once, used by every parity test):
     episode counters, truncation, ground codes): exact;
   * fp32 outputs: |got - ref| <= 1e-5 * max(1, |ref|) + 4 * spread, where
     `spread` is how far the oracle's own output moves when its inputs are
-    perturbed by one ulp (yaw +-1 ulp, positions +-1 ulp). The reference
-    evaluates cos/sin/atan2 with SLEEF on the CPU; any other implementation
-    (glibc here, ocml on the GPU) differs by up to 1 ulp, and near-tangent IR
-    rays / near-perpendicular light sensors amplify that. The spread term is
-    zero for well-conditioned elements, so for them the bar is the plain 1e-5.
+    perturbed by one ulp (yaw +-1 ulp, positions +-1 ulp) or when every
+    cos/sin/atan2/exp result inside the step is nudged by +-1 ulp. The
+    reference evaluates those with SLEEF on the CPU; any other implementation
+    (glibc here, ocml on the GPU) differs by about 1 ulp, and near-tangent IR
+    rays (ray-disc hits with r^2 - c^2 ~ 1e-7) / near-perpendicular light
+    sensors amplify that by 10^2-10^3. The spread term is zero for
+    well-conditioned elements, so for them the bar is the plain 1e-5.
   * A discrete output may differ only where a 1-ulp perturbation of the
     oracle's inputs also changes it (a threshold sits within rounding).
 """
@@ -58,16 +60,26 @@ def reference_after(fx, t: int) -> dict:
     return ref
 
 
+PERTURBATIONS = ("yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-")
+
+
+def perturbed_step(env, perturb: str | None, **kw):
+    """env.step(**kw) with one of PERTURBATIONS applied (None = plain)."""
+    if perturb:
+        what, sign = perturb[:-1], perturb[-1]
+        if what == "lm":
+            with O.libm_perturb(1 if sign == "+" else -1):
+                return env.step(**kw)
+        direction = np.inf if sign == "+" else -np.inf
+        env.s[what] = np.nextafter(env.s[what], np.float32(direction)).astype(np.float32)
+    return env.step(**kw)
+
+
 def oracle_run(fx, t: int, perturb: str | None = None) -> dict:
     env, meta = O.fixture_env(fx)
     before, kw = O.fixture_step_inputs(fx, t)
     env.load(before)
-    if perturb:
-        what, sign = perturb[:-1], perturb[-1]
-        direction = np.inf if sign == "+" else -np.inf
-        key = "yaw" if what == "yaw" else "pos"
-        env.s[key] = np.nextafter(env.s[key], np.float32(direction)).astype(np.float32)
-    obs, rew, tr = env.step(**kw)
+    obs, rew, tr = perturbed_step(env, perturb, **kw)
     out = {k: np.copy(v) for k, v in env.s.items()}
     out.update(obs=obs, reward=rew, trunc=tr)
     if meta["profile"] == "isaac":
@@ -81,7 +93,7 @@ def envelope(fx, t: int) -> tuple[dict, dict]:
     """(base oracle outputs, per-key spread / instability under 1-ulp input perturbations)."""
     base = oracle_run(fx, t)
     spread = {}
-    for p in ("yaw+", "yaw-", "pos+", "pos-"):
+    for p in PERTURBATIONS:
         o = oracle_run(fx, t, p)
         for k, v in o.items():
             if k in FLOAT_KEYS:

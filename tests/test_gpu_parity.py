@@ -128,7 +128,7 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
     s = _random_state(rng, E, N, mission)
     s["ep_len"][: E // 4] = max_len - 1          # a quarter of the envs time out this step
     ora = O.OracleEnv(mission, profile, E, N, obs_dim, discrete, max_len)
-    ora.s.update({k: np.ascontiguousarray(v) for k, v in s.items()})
+    ora.s.update({k: np.array(v, copy=True) for k, v in s.items()})   # the oracle steps in place
     ora.observe(rng.uniform(0, 1, (E, N, N)).astype(np.float32))   # consistent sensor cache
     s["cache"] = ora.s["cache"].copy()
     draws = {"rab_u_obs": rng.uniform(0, 1, (E, N, N)).astype(np.float32),
@@ -153,6 +153,8 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
     eng = SwarmEngine(mission, profile, E, N, obs_dim, discrete, max_len, 1, 0, 0, gpu_device)
     eng.reset()
     eng.load_state(s)
+    for k, v in s.items():
+        assert k == "cache" or not np.shares_memory(v, ora.s[k])
     replay = {"rab_uniform": _dev(draws["rab_u_obs"][None], np.float32, gpu_device),
               "rab_uniform_dispatch": _dev(draws["rab_u_dispatch"][None], np.float32, gpu_device),
               "turn_steps": _dev(draws["turns"][None], np.int32, gpu_device),
@@ -172,12 +174,10 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
         ref.pop("cache")
     # envelope from 1-ulp perturbed oracle runs of the same inputs
     spread = {}
-    for p in ("yaw+", "yaw-", "pos+", "pos-"):
+    for p in parity.PERTURBATIONS:
         o2 = O.OracleEnv(mission, profile, E, N, obs_dim, discrete, max_len)
         o2.s.update({k: np.copy(v) for k, v in s.items()})
-        key = "yaw" if p.startswith("yaw") else "pos"
-        o2.s[key] = np.nextafter(o2.s[key], np.float32(np.inf if p[-1] == "+" else -np.inf)).astype(np.float32)
-        ob2, rw2, tr2 = o2.step(acts, ovr, draws)
+        ob2, rw2, tr2 = parity.perturbed_step(o2, p, actions=acts, override=ovr, draws=draws)
         out2 = dict(o2.s, obs=ob2, reward=rw2, trunc=tr2)
         for k, v in out2.items():
             if k not in ref:
@@ -195,18 +195,19 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
 #  Philox path: determinism, sharding invariance, decision fusion, statistics
 # --------------------------------------------------------------------------
 
-def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed=7, max_len=23):
+def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed=7, max_len=23, total=None):
     from SwarmACB_isaac.engine import SwarmEngine
 
     eng = SwarmEngine(mission, "isaac", E, 20, 24, discrete, max_len, 1, offset, seed, device)
     eng.reset()
     g = torch.Generator(device="cpu").manual_seed(1)
     outs = []
+    total = total or (E + offset)   # actions are drawn for the global batch, then sliced to this shard
     for k in range(steps):
         if discrete:
-            a = torch.randint(0, 6, (E + offset, 20), generator=g, dtype=torch.int32)[offset:].contiguous()
+            a = torch.randint(0, 6, (total, 20), generator=g, dtype=torch.int32)[offset:offset + E].contiguous()
         else:
-            a = (torch.randn(E + offset, 20, 2, generator=g).clamp(-3, 3) / 3)[offset:].contiguous()
+            a = (torch.randn(total, 20, 2, generator=g).clamp(-3, 3) / 3)[offset:offset + E].contiguous()
         obs, rew, tr = eng.step(a.to(device), n_sub)
         outs.append((obs.cpu().clone(), rew.cpu().clone(), tr.cpu().clone()))
     st = eng.dump_state()
@@ -217,9 +218,9 @@ def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed
 @pytest.mark.parametrize("discrete", [False, True])
 def test_sharding_invariance_bitwise(discrete, gpu_device):
     """Envs split over two engines (env_offset) reproduce one engine bit for bit."""
-    full, st_full = _run(gpu_device, 6, 0, 30, 1, discrete=discrete)
-    lo, st_lo = _run(gpu_device, 3, 0, 30, 1, discrete=discrete)
-    hi, st_hi = _run(gpu_device, 3, 3, 30, 1, discrete=discrete)
+    full, st_full = _run(gpu_device, 6, 0, 30, 1, discrete=discrete, total=6)
+    lo, st_lo = _run(gpu_device, 3, 0, 30, 1, discrete=discrete, total=6)
+    hi, st_hi = _run(gpu_device, 3, 3, 30, 1, discrete=discrete, total=6)
     for (of, rf, tf), (ol, rl, tl), (oh, rh, th) in zip(full, lo, hi):
         assert torch.equal(of[:3], ol) and torch.equal(of[3:], oh)
         assert torch.equal(rf, torch.cat([rl, rh])) and torch.equal(tf, torch.cat([tl, th]))
@@ -316,6 +317,9 @@ def test_full_size_homing_properties(gpu_device):
     # after the auto-reset every robot is back in the spawn region, inside the arena
     px, py = eng.x.cpu().numpy(), eng.y.cpu().numpy()
     assert (np.hypot(px, py - 0.7) < 0.8 + 0.2).mean() > 0.999
-    assert (np.hypot(px, py) < 1.2357 - 0.035).all()
+    # inside the dodecagon: signed distance to every face >= the robot radius (DG:1048-1078)
+    ang = (np.arange(12) + 1) * 2 * np.pi / 12          # face mid-angles (vertices at 2*pi*i/12 + pi/12)
+    sd = 1.2357 - (px[:, None] * np.cos(ang) + py[:, None] * np.sin(ang))
+    assert (sd >= 0.035).all(), sd.min()
     assert (eng.episode_length.cpu().numpy() == 0).all()
     eng.close()
