@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--decision-period", type=int, default=5)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--wg-waves", type=int, default=0, help="waves per workgroup (1, 2, 4; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
     return ap.parse_args()
 
@@ -112,7 +113,8 @@ def main():
     from SwarmACB_isaac.engine import SwarmEngine
 
     E, dp = args.envs, args.decision_period
-    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, rank * E, args.seed, dev)
+    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, rank * E, args.seed, dev,
+                      wg_waves=args.wg_waves or None)
     obs, rew, tr = eng.reset()
     out = (obs, rew, tr)
 
@@ -174,6 +176,7 @@ def main():
                 "num_agents": N_AGENTS,
                 "global_envs": world * E,
                 "decision_period": dp,
+                "wg_waves": args.wg_waves or "default",
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,
             },

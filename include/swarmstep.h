@@ -72,7 +72,7 @@ typedef struct {
     int32_t discrete_actions;     /* 1: action = behaviour-module id (int32); 0: wheels (float2) */
     int32_t max_episode_length;   /* steps; isaac ceil(episode_length_s/(dt*decimation)) */
     int32_t decimation;           /* isaac physics substeps per env.step (DGC:97) */
-    int32_t reserved0;
+    int32_t wg_waves;             /* waves cooperating on one workgroup's arenas: 1, 2, 4 (0 = auto) */
     int64_t env_offset;           /* global index of local env 0 (multi-GPU sharding) */
     uint64_t seed;                /* Philox key for all in-kernel randomness */
 } swarm_params_t;

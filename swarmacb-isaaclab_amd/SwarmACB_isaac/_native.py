@@ -25,7 +25,7 @@ class SwarmParams(C.Structure):
         ("abi_version", C.c_int32), ("mission", C.c_int32), ("profile", C.c_int32),
         ("num_envs", C.c_int32), ("num_agents", C.c_int32), ("obs_dim", C.c_int32),
         ("discrete_actions", C.c_int32), ("max_episode_length", C.c_int32), ("decimation", C.c_int32),
-        ("reserved0", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
+        ("wg_waves", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
     ]
 
 

@@ -80,6 +80,7 @@ void build_geom(const swarm_params_t& p, Geom& g) {
     g.max_len = p.max_episode_length;
     g.decimation = p.decimation > 0 ? p.decimation : 1;
     g.apb = 64 / p.num_agents;
+    g.waves = p.wg_waves > 0 ? p.wg_waves : 4;
     g.seed_lo = (uint32_t)p.seed;
     g.seed_hi = (uint32_t)(p.seed >> 32);
     g.env_off_lo = (uint32_t)p.env_offset;
@@ -240,6 +241,10 @@ void build_geom(const swarm_params_t& p, Geom& g) {
     g.two_pi_f = (float)(2.0 * PI);
     g.half_pi_f = (float)(PI * 0.5);
     g.critic_radius = 1.20f;
+    // fl(sqrt(s)) < x requires sqrt(s) < x, i.e. s < x^2; the margin keeps the
+    // float pre-filter a strict superset of the exact test (the kernels re-check).
+    g.min_dist2_hi = (float)((double)g.min_dist * g.min_dist * (1.0 + 1.0 / 1048576.0));
+    g.rab_range2_hi = (float)((double)g.rab_range * g.rab_range * (1.0 + 1.0 / 1048576.0));
 }
 
 DevState dev_state(const swarm_state_t* s) {
@@ -295,6 +300,7 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     if (p->num_envs < 1 || p->num_agents < 1 || p->num_agents > SWARM_MAX_AGENTS) return SWARM_ERR_ARG;
     if (p->obs_dim != 24 && p->obs_dim != 4) return SWARM_ERR_ARG;
     if (p->max_episode_length < 1 || p->decimation < 0 || p->env_offset < 0) return SWARM_ERR_ARG;
+    if (p->wg_waves != 0 && p->wg_waves != 1 && p->wg_waves != 2 && p->wg_waves != 4) return SWARM_ERR_ARG;
     swarm_handle_t* h = new (std::nothrow) swarm_handle_t();
     if (!h) return SWARM_ERR_ARG;
     h->p = *p;

@@ -26,6 +26,7 @@ struct Geom {
     int32_t mission, profile, N, E;
     int32_t obs_dim, discrete, max_len, decimation;
     int32_t apb;            // arenas per 64-lane wave (= 64 / N)
+    int32_t waves;          // cooperating waves per workgroup (1, 2 or 4)
     int32_t nseg, nint;     // raycast segments (arena 12 + internal), internal walls
     int32_t has_light;
     uint32_t seed_lo, seed_hi;
@@ -67,6 +68,8 @@ struct Geom {
 
     // ---- scalar constants ----
     float r_robot, min_dist, r2, max_speed, wheelbase, dt;
+    // squared-distance pre-filters: s >= x2_hi guarantees fl(sqrt(s)) >= x (x^2 (1 + 2^-20))
+    float min_dist2_hi, rab_range2_hi;
     float prox_range, rab_range, rab_loss, unity, light_thr, light_int, alpha, prox_thr;
     float pi_f, two_pi_f, half_pi_f, critic_radius;
 };

@@ -1,0 +1,14 @@
+// swarm_mission.hip — one translation unit per mission (-DSWARM_MISSION_ID=0..4),
+// so the 5 x {profile, action kind, N, waves} kernel instantiations compile in parallel.
+#include "swarm_step_impl.h"
+
+#ifndef SWARM_MISSION_ID
+#error "compile with -DSWARM_MISSION_ID=<0..4>"
+#endif
+
+namespace swarm {
+template void launch_step_m<SWARM_MISSION_ID>(const Geom&, const DevState&, const void*, const float*, const DevOut&,
+                                              const DevReplay&, uint64_t, int, uint64_t, hipStream_t);
+template void launch_reset_m<SWARM_MISSION_ID>(const Geom&, const DevState&, const uint8_t*, const DevOut&,
+                                               const DevReplay&, uint64_t, hipStream_t);
+}  // namespace swarm

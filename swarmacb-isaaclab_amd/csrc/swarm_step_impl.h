@@ -1,13 +1,24 @@
-// swarm_kernels.hip — fused e-puck env step for CDNA4 (gfx950).
+// swarm_step_impl.h — fused e-puck env step for CDNA4 (gfx950).
 //
-// One 64-lane wave per workgroup holds floor(64/N) complete arenas (3 for the
-// reference's N = 20 robots: lanes 0-19, 20-39, 40-59), one robot per lane.
-// Everything a robot needs from its arena-mates (positions, "inside" flags)
-// is exchanged through a 64-entry LDS tile; per-arena integer reductions
-// (goal / target / shelter / nest counts, K+ and K-) are wave ballots masked
-// to the arena's lane range + popcount. State lives in registers for all
-// substeps of a launch (the ML-Agents decision period), so HBM sees each state
-// word once per launch, the action once, and the observation once per substep.
+// Device code + launch templates; swarm_mission.hip compiles it once per
+// mission (parallel translation units), swarm_dispatch.hip picks the mission.
+//
+// A workgroup holds floor(64/N) complete arenas (3 for the reference's N = 20
+// robots: lanes 0-19, 20-39, 40-59 of a wave), one robot per lane, and runs
+// W cooperating waves over those same arenas. Every wave carries the full
+// per-robot state in registers (bit-identical in all W waves); the O(N) work
+// per robot — neighbour loops of the contact solver and range-and-bearing,
+// proximity rays against walls and robots — is split into W contiguous
+// neighbour chunks / segment subsets, and the partial sums (fixed wave order)
+// or maxima are exchanged through LDS. W multiplies the waves in flight: the
+// reference workload (20 x 4096 envs) is only 1366 single waves, 1.3 per SIMD,
+// which leaves a latency-bound kernel with nothing to hide behind.
+// Positions are exchanged through a 64-entry LDS tile; per-arena integer
+// reductions (goal / target / shelter / nest counts, K+ and K-) are wave
+// ballots masked to the arena's lane range + popcount. State lives in
+// registers for all substeps of a launch (the ML-Agents decision period), so
+// HBM sees each state word once per launch, the action once, and the
+// observation once per substep.
 //
 // Reference semantics (file:line of /root/reference):
 //   integrate        epuck_sensors.py:592-617, directional_gate_env.py:816-826 / manual_control.py:355-366
@@ -18,11 +29,18 @@
 //                    foraging_env.py:127-138, sheltering_env.py:157-160 / manual_control.py:372-423
 //   reset            directional_gate_env.py:1215-1273, foraging_env.py:140-151 / manual_control.py:245-269
 //   observation      directional_gate_env.py:1118-1148, epuck_sensors.py:507-539
+#pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "swarm_geom.h"
 #include "swarm_launch.h"
+
+// Timing-only ablation switches (tools/ablate.sh builds variants with
+// -DSWARM_ABLATE=mask; results are then WRONG by design). 0 in every product build.
+#ifndef SWARM_ABLATE
+#define SWARM_ABLATE 0
+#endif
 
 namespace swarm {
 
@@ -51,6 +69,20 @@ __device__ __forceinline__ uint4 rng4(const Geom& g, uint32_t genv, uint32_t rob
 // torch-style float uniform from 24 random bits: [0, 1)
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
+// Five independent 24-bit uniforms from one Philox block (120 of its 128 bits):
+// the packet-loss draws of neighbours j = 5*blk .. 5*blk+4.
+__device__ __forceinline__ float u01_of5(const uint4& r, int w) {
+    uint32_t v;
+    switch (w) {
+    case 0: v = r.x >> 8; break;
+    case 1: v = r.y >> 8; break;
+    case 2: v = r.z >> 8; break;
+    case 3: v = r.w >> 8; break;
+    default: v = (r.x & 0xFFu) | ((r.y & 0xFFu) << 8) | ((r.z & 0xFFu) << 16); break;
+    }
+    return (float)v * (1.0f / 16777216.0f);
+}
+
 __device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
@@ -78,17 +110,29 @@ __device__ __forceinline__ uint32_t fsm_put(Fsm m, int sh) {
 //  Per-lane context
 // ---------------------------------------------------------------------------
 struct Lane {
+    int N;                    // robots per arena (a compile-time constant for the N = 20 specialisation)
+    int wv;                   // wave index inside the workgroup (wave-uniform, in an SGPR)
+    int j0, j1;               // this wave's neighbour chunk [j0, j1)
     int lane, a, i, env, ab;  // ab = LDS base of this lane's arena
     bool valid;
     uint32_t genv;
     unsigned long long amask;  // ballot bits of this lane's arena
 };
 
-struct Tile {                 // LDS arena tiles of one wave
-    float x[64];
-    float y[64];
+// LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
+// broadcast within an arena) and W x 4 float4 partial slots per lane.
+// Slot use: 0 contact-solver sums, 0-1 proximity maxima, 2-3 range-and-bearing sums.
+template <int W>
+struct Shared {
+    float2 xy[64];
     int ins[64];
+    float4 red[W > 1 ? W : 1][4][64];
 };
+
+template <int W>
+__device__ __forceinline__ void sync_wg() {
+    __syncthreads();
+}
 
 __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     const unsigned long long m = __ballot(pred);
@@ -101,6 +145,7 @@ __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
 
 // DG:1048-1078 — inward push summed over all penetrated faces (Jacobi).
 __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
+    if (SWARM_ABLATE & 8) return;
     float tx = 0.0f, ty = 0.0f;
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
@@ -127,26 +172,35 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 }
 
 // DG:1080-1112 / MC:555-571 — Jacobi half-overlap push over pairs i<j.
-__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Tile& T, float& x, float& y) {
-    T.x[L.lane] = x;
-    T.y[L.lane] = y;
-    __syncthreads();
-    // candidate pairs (cheap pass), then the exact terms only for overlapping pairs
+// Each wave sums its neighbour chunk; the W partial sums are added in wave order.
+template <int W, int C>
+__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y) {
+    if (SWARM_ABLATE & 4) return;
+    if (L.wv == 0) S.xy[L.lane] = make_float2(x, y);
+    sync_wg<W>();
+    // candidate pairs from the squared distance (a superset: s >= md2_hi implies
+    // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
     unsigned long long cand = 0;
-    for (int j = 0; j < g.N; ++j) {
-        const float dx = x - T.x[L.ab + j], dy = y - T.y[L.ab + j];
-        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
-        if (j != L.i && g.min_dist - dist > 0.0f) cand |= 1ull << j;
+#pragma unroll
+    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+        const int j = L.j0 + jj;
+        if (C == 0 && j >= L.j1) break;
+        if (C > 0 && j >= L.j1) continue;
+        const float2 p = S.xy[L.ab + j];
+        const float dx = x - p.x, dy = y - p.y;
+        const float s = dx * dx + dy * dy + 1e-8f;
+        if (j != L.i && s < g.min_dist2_hi) cand |= 1ull << j;
     }
-    const bool any = __any(cand != 0ull);
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
-    if (any) {
+    {
         while (cand) {
             const int j = __builtin_ctzll(cand);
             cand &= cand - 1ull;
-            const float dx = x - T.x[L.ab + j], dy = y - T.y[L.ab + j];
+            const float2 p = S.xy[L.ab + j];
+            const float dx = x - p.x, dy = y - p.y;
             const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
             const float ov = g.min_dist - dist;
+            if (!(ov > 0.0f)) continue;
             const float nx = dx / (dist + 1e-8f), ny = dy / (dist + 1e-8f);
             if (j > L.i) {  // row term of pair (i, j)
                 rx += ov * nx * 0.5f;
@@ -157,11 +211,27 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Tile& 
             }
         }
     }
-    __syncthreads();
-    if (any) {
-        x = (x + rx) - cx;
-        y = (y + ry) - cy;
+    if constexpr (W > 1) {
+        S.red[L.wv][0][L.lane] = make_float4(rx, ry, cx, cy);
+        sync_wg<W>();
+        float4 a = S.red[0][0][L.lane];
+#pragma unroll
+        for (int k = 1; k < W; ++k) {
+            const float4 b = S.red[k][0][L.lane];
+            a.x += b.x;
+            a.y += b.y;
+            a.z += b.z;
+            a.w += b.w;
+        }
+        rx = a.x;
+        ry = a.y;
+        cx = a.z;
+        cy = a.w;
+    } else {
+        sync_wg<W>();
     }
+    x = (x + rx) - cx;
+    y = (y + ry) - cy;
 }
 
 // DG:658-705 (DirGate and XOR, which keeps the base-class version)
@@ -276,8 +346,8 @@ __device__ __forceinline__ void capsules(const Geom& g, float& x, float& y, bool
 }
 
 // DG:874-896 — pre pass, solver iterations, post pass.
-template <int MISSION>
-__device__ __forceinline__ void resolve_collisions(const Geom& g, const Lane& L, Tile& T, float& x, float& y,
+template <int MISSION, int W, int C>
+__device__ __forceinline__ void resolve_collisions(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y,
                                                    bool has_prev, float qx, float qy) {
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     walls_dg(g, x, y);
@@ -288,7 +358,7 @@ __device__ __forceinline__ void resolve_collisions(const Geom& g, const Lane& L,
     gate_walls<MISSION, ISAAC>(g, x, y);
     for (int it = 0; it < 4; ++it) {                     // collision_solver_iterations (DGC:127)
         const float bx = x, by = y;
-        robots_push(g, L, T, x, y);
+        robots_push<W, C>(g, L, S, x, y);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             anti_tunnel(g, x, y, bx, by);
@@ -339,18 +409,16 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
     float pv, pa, lv, la, ax, ay;
 };
 
-// ES:85-142, 184-293 : writes the 8 readings to prox[] and the aggregate.
-__device__ __forceinline__ void proximity(const Geom& g, const Lane& L, const Tile& T, float x, float y, float cyw,
-                                          float syw, float prox[8], float& pv, float& pa) {
-    float rdx[8], rdy[8];
+// ES:85-142, 184-293: per-ray readings (max over segments and robot discs).
+// Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
+// all 8 rays; max is order-free, so the W partial maxima combine exactly.
+template <int W, int C>
+__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const Shared<W>& S, float x, float y,
+                                                  const float rdx[8], const float rdy[8], float prox[8]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
-        rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
-        prox[k] = 0.0f;
-    }
+    for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length
-    for (int s = 0; s < g.nseg; ++s) {
+    for (int s = L.wv; s < g.nseg; s += W) {
         bool near;
         if (s < 12) {
             const float sd = (x - g.face_px[s]) * g.face_nx[s] + (y - g.face_py[s]) * g.face_ny[s];
@@ -379,14 +447,20 @@ __device__ __forceinline__ void proximity(const Geom& g, const Lane& L, const Ti
     }
     // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
     unsigned long long cand = 0;
-    for (int j = 0; j < g.N; ++j) {
-        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+#pragma unroll
+    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+        const int j = L.j0 + jj;
+        if (C == 0 && j >= L.j1) break;
+        if (C > 0 && j >= L.j1) continue;
+        const float2 p = S.xy[L.ab + j];
+        const float dx = p.x - x, dy = p.y - y;
         if (j != L.i && dx * dx + dy * dy <= 0.0200f) cand |= 1ull << j;
     }
     while (cand) {
         const int j = __builtin_ctzll(cand);
         cand &= cand - 1ull;
-        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        const float2 p = S.xy[L.ab + j];
+        const float dx = p.x - x, dy = p.y - y;
         const float dsq = dx * dx + dy * dy;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -399,6 +473,10 @@ __device__ __forceinline__ void proximity(const Geom& g, const Lane& L, const Ti
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
     }
+}
+
+// ES:134-142: vector sum of the readings -> (value, angle)
+__device__ __forceinline__ void proximity_aggregate(const Geom& g, const float prox[8], float& pv, float& pa) {
     float sx = 0.0f, sy = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -440,19 +518,32 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
     la = above ? ang : 0.0f;
 }
 
-// ES:382-501 — range-and-bearing with line of sight and packet loss.
-// u_replay: this robot's row of N uniforms, or nullptr (Philox stream `purpose`).
-__device__ __forceinline__ void rab(const Geom& g, const Lane& L, const Tile& T, float x, float y, float cyw, float syw,
-                                    const float* u_replay, uint32_t purpose, uint64_t tick, float& zt, float r4[4],
-                                    float& ax_out, float& ay_out) {
+// ES:382-501 — range-and-bearing with line of sight and packet loss: the
+// partial sums (kept count, 1/d-weighted bearing, attraction) over this wave's
+// neighbour chunk. u_replay: this robot's row of N uniforms, or nullptr
+// (Philox stream `purpose`, one block per 5 neighbours).
+template <int C>
+__device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv, float x,
+                                            float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
+                                            uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy) {
+    // in-range candidates from the squared distance (superset), exact test in the loop
     unsigned long long cand = 0;
-    for (int j = 0; j < g.N; ++j) {
-        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
-        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
-        if (j != L.i && dist < g.rab_range) cand |= 1ull << j;
+#pragma unroll
+    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+        const int j = L.j0 + jj;
+        if (C == 0 && j >= L.j1) break;
+        if (C > 0 && j >= L.j1) continue;
+        const float2 p = xy[L.ab + j];
+        const float dx = p.x - x, dy = p.y - y;
+        const float s = dx * dx + dy * dy + 1e-8f;
+        if (j != L.i && s < g.rab_range2_hi) cand |= 1ull << j;
     }
-    const bool me_in = T.ins[L.lane] != 0;
-    float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
+    const bool me_in = insv[L.lane] != 0;
+    n = 0.0f;
+    wx = 0.0f;
+    wy = 0.0f;
+    axx = 0.0f;
+    ayy = 0.0f;
     int blk = -1;
     uint4 rb = make_uint4(0, 0, 0, 0);
     while (cand) {
@@ -462,19 +553,21 @@ __device__ __forceinline__ void rab(const Geom& g, const Lane& L, const Tile& T,
         if (u_replay) {
             uu = u_replay[j];
         } else {
-            if ((j >> 2) != blk) {
-                blk = j >> 2;
+            const int b = j / 5;
+            if (b != blk) {
+                blk = b;
                 rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
             }
-            const uint32_t w = (j & 3) == 0 ? rb.x : ((j & 3) == 1 ? rb.y : ((j & 3) == 2 ? rb.z : rb.w));
-            uu = u01(w);
+            uu = u01_of5(rb, j - 5 * b);
         }
         if (!(uu >= g.rab_loss)) continue;
-        const float dx = T.x[L.ab + j] - x, dy = T.y[L.ab + j] - y;
+        const float2 p = xy[L.ab + j];
+        const float dx = p.x - x, dy = p.y - y;
         const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        if (!(dist < g.rab_range)) continue;
         // line of sight (ES:462-501): arena faces can only block if an end point is
         // not strictly inside the convex arena; internal walls are always tested.
-        const bool test_arena = !(me_in && T.ins[L.ab + j] != 0);
+        const bool test_arena = !(me_in && insv[L.ab + j] != 0);
         const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
         bool blocked = false;
         for (int s = test_arena ? 0 : 12; s < g.nseg; ++s) {
@@ -501,12 +594,15 @@ __device__ __forceinline__ void rab(const Geom& g, const Lane& L, const Tile& T,
         axx += aw * cb;
         ayy += aw * sb;
     }
+}
+
+// ES:452-460: ztilde and the four body-frame projections from the sums
+__device__ __forceinline__ void rab_finish(const Geom& g, float n, float wx, float wy, float& zt, float r4[4]) {
     zt = 1.0f - 2.0f / (1.0f + expf(n));
 #pragma unroll
     for (int k = 0; k < 4; ++k) r4[k] = wx * g.rab_cos[k] + wy * g.rab_sin[k];
-    ax_out = axx;
-    ay_out = ayy;
 }
+
 
 // ---------------------------------------------------------------------------
 //  Behaviour modules (BM:50-574)
@@ -619,37 +715,121 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE>
-__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Tile& T, float x, float y, float yaw,
-                                        const float* u_replay, uint64_t tick, float* obs, Agg& agg) {
-    // publish positions and the strictly-inside flag used by the LOS shortcut
+// Publishes positions + "strictly inside the arena" flags (LOS shortcut).
+template <int W>
+__device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<W>& S, float x, float y) {
     bool ins = true;
 #pragma unroll
     for (int k = 0; k < 12; ++k)
         ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
-    T.x[L.lane] = x;
-    T.y[L.lane] = y;
-    T.ins[L.lane] = ins ? 1 : 0;
-    __syncthreads();
+    if (L.wv == 0) {
+        S.xy[L.lane] = make_float2(x, y);
+        S.ins[L.lane] = ins ? 1 : 0;
+    }
+    sync_wg<W>();
+}
+
+// Range-and-bearing sums over all neighbours: this wave's chunk + the other
+// waves' partials (slots 2-3), added in wave order. Must follow publish().
+// With `with_prox`, also max-combines the proximity readings (slots 0-1).
+template <int W, int C>
+__device__ __forceinline__ void combine(const Lane& L, Shared<W>& S, bool with_prox, float prox[8], float& n,
+                                        float& wx, float& wy, float& axx, float& ayy) {
+    if constexpr (W > 1) {
+        if (with_prox) {
+            S.red[L.wv][0][L.lane] = make_float4(prox[0], prox[1], prox[2], prox[3]);
+            S.red[L.wv][1][L.lane] = make_float4(prox[4], prox[5], prox[6], prox[7]);
+        }
+        S.red[L.wv][2][L.lane] = make_float4(n, wx, wy, axx);
+        S.red[L.wv][3][L.lane].x = ayy;
+        sync_wg<W>();
+        if (with_prox) {
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                if (k == L.wv) continue;
+                const float4 a = S.red[k][0][L.lane], b = S.red[k][1][L.lane];
+                prox[0] = fmaxf(prox[0], a.x);
+                prox[1] = fmaxf(prox[1], a.y);
+                prox[2] = fmaxf(prox[2], a.z);
+                prox[3] = fmaxf(prox[3], a.w);
+                prox[4] = fmaxf(prox[4], b.x);
+                prox[5] = fmaxf(prox[5], b.y);
+                prox[6] = fmaxf(prox[6], b.z);
+                prox[7] = fmaxf(prox[7], b.w);
+            }
+        }
+        float4 s = S.red[0][2][L.lane];
+        float sa = S.red[0][3][L.lane].x;
+#pragma unroll
+        for (int k = 1; k < W; ++k) {
+            const float4 b = S.red[k][2][L.lane];
+            s.x += b.x;
+            s.y += b.y;
+            s.z += b.z;
+            s.w += b.w;
+            sa += S.red[k][3][L.lane].x;
+        }
+        n = s.x;
+        wx = s.y;
+        wy = s.z;
+        axx = s.w;
+        ayy = sa;
+    } else {
+        sync_wg<W>();
+    }
+}
+
+// ---------------------------------------------------------------------------
+//  Observation pass (writes obs + returns the aggregates for the cache)
+// ---------------------------------------------------------------------------
+template <int MISSION, int PROFILE, int W, int C>
+__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float yaw,
+                                        const float* u_replay, uint64_t tick, float* obs, Agg& agg) {
+    publish<W>(g, L, S, x, y);
     float syw, cyw;
     sincosf(yaw, &syw, &cyw);
+    float rdx[8], rdy[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
+        rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
+    }
     float prox[8], lt[8], r4[4], zt;
-    proximity(g, L, T, x, y, cyw, syw, prox, agg.pv, agg.pa);
+    float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
+    if (SWARM_ABLATE & 2) {
+        for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
+    } else {
+        proximity_partial<W, C>(g, L, S, x, y, rdx, rdy, prox);
+    }
+    if (!(SWARM_ABLATE & 1))
+        rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy);
+    combine<W, C>(L, S, true, prox, n, wx, wy, axx, ayy);
+    proximity_aggregate(g, prox, agg.pv, agg.pa);
     light(g, x, y, cyw, syw, lt, agg.lv, agg.la);
-    rab(g, L, T, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, zt, r4, agg.ax, agg.ay);
-    __syncthreads();
+    rab_finish(g, n, wx, wy, zt, r4);
+    agg.ax = axx;
+    agg.ay = ayy;
     if (L.valid && obs) {
         const float gv = 0.5f * (float)ground_code<MISSION, PROFILE>(g, x, y);
-        float* o = obs + ((size_t)L.env * g.N + L.i) * g.obs_dim;
+        float* o = obs + ((size_t)L.env * L.N + L.i) * g.obs_dim;
         if (g.obs_dim == 24) {
             float4* o4 = reinterpret_cast<float4*>(o);
-            o4[0] = make_float4(prox[0], prox[1], prox[2], prox[3]);
-            o4[1] = make_float4(prox[4], prox[5], prox[6], prox[7]);
-            o4[2] = make_float4(lt[0], lt[1], lt[2], lt[3]);
-            o4[3] = make_float4(lt[4], lt[5], lt[6], lt[7]);
-            o4[4] = make_float4(gv, gv, gv, zt);
-            o4[5] = make_float4(r4[0], r4[1], r4[2], r4[3]);
-        } else {
+            // chunk c of the 24-D row is stored by wave c % W
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                if (c % W != L.wv) continue;
+                float4 v;
+                switch (c) {
+                case 0: v = make_float4(prox[0], prox[1], prox[2], prox[3]); break;
+                case 1: v = make_float4(prox[4], prox[5], prox[6], prox[7]); break;
+                case 2: v = make_float4(lt[0], lt[1], lt[2], lt[3]); break;
+                case 3: v = make_float4(lt[4], lt[5], lt[6], lt[7]); break;
+                case 4: v = make_float4(gv, gv, gv, zt); break;
+                default: v = make_float4(r4[0], r4[1], r4[2], r4[3]); break;
+                }
+                o4[c] = v;
+            }
+        } else if (L.wv == 0) {
             *reinterpret_cast<float4*>(o) = make_float4(gv, gv, gv, zt);
         }
     }
@@ -657,20 +837,15 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Tile& T, f
 
 // standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
 // proximity/light aggregates equal those of the previous observation (same pose).
-__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Tile& T, float x, float y, float yaw,
+template <int W, int C>
+__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float yaw,
                                          const float* u_replay, uint64_t tick, float& ax, float& ay) {
-    bool ins = true;
-#pragma unroll
-    for (int k = 0; k < 12; ++k)
-        ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
-    T.x[L.lane] = x;
-    T.y[L.lane] = y;
-    T.ins[L.lane] = ins ? 1 : 0;
-    __syncthreads();
-    float syw, cyw, zt, r4[4];
+    publish<W>(g, L, S, x, y);
+    float syw, cyw;
     sincosf(yaw, &syw, &cyw);
-    rab(g, L, T, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, zt, r4, ax, ay);
-    __syncthreads();
+    float n, wx, wy;
+    rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax, ay);
+    combine<W, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
 }
 
 // ---------------------------------------------------------------------------
@@ -682,7 +857,7 @@ __device__ __forceinline__ void spawn_isaac(const Geom& g, const Lane& L, const 
                                             float& y, float& yaw) {
     const bool rej = g.sp_rad > 0.0f;
     const int K = rp.spawn ? rp.spawn_k : (rej ? g.sp_attempts + 1 : 1);
-    const size_t q = (size_t)L.env * g.N + L.i;
+    const size_t q = (size_t)L.env * L.N + L.i;
     uint4 rb = make_uint4(0, 0, 0, 0);
     for (int k = 0; k < K; ++k) {
         if (k > 0) {
@@ -691,7 +866,7 @@ __device__ __forceinline__ void spawn_isaac(const Geom& g, const Lane& L, const 
         }
         float u0, u1;
         if (rp.spawn) {
-            const float* p = rp.spawn + (((size_t)k * g.E) * g.N + q) * 2;
+            const float* p = rp.spawn + (((size_t)k * g.E) * L.N + q) * 2;
             u0 = p[0];
             u1 = p[1];
         } else {
@@ -713,9 +888,9 @@ template <int MISSION>
 __device__ __forceinline__ void spawn_mc(const Geom& g, const Lane& L, const DevReplay& rp, uint64_t tick, float& x,
                                          float& y, float& yaw) {
     float ur, ut, uy;
-    const size_t q = (size_t)L.env * g.N + L.i;
+    const size_t q = (size_t)L.env * L.N + L.i;
     if (rp.spawn) {
-        const size_t EN = (size_t)g.E * g.N;
+        const size_t EN = (size_t)g.E * L.N;
         ur = rp.spawn[q];
         ut = rp.spawn[EN + q];
         uy = rp.spawn[2 * EN + q];
@@ -779,29 +954,40 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 // ---------------------------------------------------------------------------
 //  The fused step kernel
 // ---------------------------------------------------------------------------
+// NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
+// every neighbour loop has a compile-time trip count and is fully unrolled.
+template <int NA, int W>
 __device__ __forceinline__ Lane make_lane(const Geom& g) {
     Lane L;
-    L.lane = threadIdx.x;
-    L.a = L.lane / g.N;
-    L.i = L.lane - L.a * g.N;
-    L.env = blockIdx.x * g.apb + L.a;
-    L.valid = (L.a < g.apb) && (L.env < g.E);
-    L.ab = (L.a < g.apb ? L.a : 0) * g.N;
+    L.N = NA > 0 ? NA : g.N;
+    const int apb = NA > 0 ? 64 / (NA > 0 ? NA : 1) : g.apb;
+    L.lane = threadIdx.x & 63;
+    L.wv = W > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+    const int chunk = (L.N + W - 1) / W;
+    L.j0 = L.wv * chunk;
+    L.j1 = min(L.N, L.j0 + chunk);
+    L.a = L.lane / L.N;
+    L.i = L.lane - L.a * L.N;
+    L.env = blockIdx.x * apb + L.a;
+    L.valid = (L.a < apb) && (L.env < g.E);
+    L.ab = (L.a < apb ? L.a : 0) * L.N;
     const uint64_t goff = ((uint64_t)g.env_off_hi << 32) | g.env_off_lo;
     L.genv = (uint32_t)(goff + (uint64_t)(L.env < g.E ? L.env : 0));
-    const unsigned long long m = g.N >= 64 ? ~0ull : ((1ull << g.N) - 1ull);
-    L.amask = (L.a < g.apb) ? (m << L.ab) : 0ull;
+    const unsigned long long m = L.N >= 64 ? ~0ull : ((1ull << L.N) - 1ull);
+    L.amask = (L.a < apb) ? (m << L.ab) : 0ull;
     return L;
 }
 
-template <int MISSION, int PROFILE, bool DISCRETE>
-__global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
-                                                  const float* __restrict__ ovr, const DevOut out, const DevReplay rp,
-                                                  uint64_t tick0, int n_sub, uint64_t reset_any) {
-    __shared__ Tile T;
-    const Lane L = make_lane(g);
-    const size_t q = L.valid ? (size_t)L.env * g.N + L.i : 0;
-    const size_t EN = (size_t)g.E * g.N;
+template <int MISSION, int PROFILE, bool DISCRETE, int NA, int W>
+__global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
+                                                      const float* __restrict__ ovr, const DevOut out,
+                                                      const DevReplay rp, uint64_t tick0, int n_sub,
+                                                      uint64_t reset_any) {
+    constexpr int C = NA > 0 ? (NA + W - 1) / W : 0;   // neighbour chunk per wave (0 = runtime)
+    __shared__ Shared<W> S;
+    const Lane L = make_lane<NA, W>(g);
+    const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
+    const size_t EN = (size_t)g.E * L.N;
 
     // ---- load state (invalid lanes keep harmless values) ----
     float x = 0.0f, y = 0.0f, yaw = 0.0f, wl = 0.0f, wr = 0.0f;
@@ -849,16 +1035,16 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
 
     for (int s = 0; s < n_sub; ++s) {
         const uint64_t tick = tick0 + (uint64_t)s;
-        const size_t NN = (size_t)g.N * g.N;
-        const float* u_obs = rp.rab ? rp.rab + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * g.N : nullptr;
+        const size_t NN = (size_t)L.N * L.N;
+        const float* u_obs = rp.rab ? rp.rab + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
         TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, EN, q, tick};
 
         // ------------------------------ actions ------------------------------
         float lw, rw;
         if constexpr (PROFILE == STANDALONE) {
-            const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * g.N
+            const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
                                         : nullptr;
-            rab_only(g, L, T, x, y, yaw, u_d, tick, cache.ax, cache.ay);
+            rab_only<W, C>(g, L, S, x, y, yaw, u_d, tick, cache.ax, cache.ay);
             if constexpr (DISCRETE) {
                 dispatch(g, L, mod, cache, 0.0f, 0.0f, fsm, ts, lw, rw);   // previous = zeros (MC:744-747)
             } else {
@@ -897,14 +1083,15 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
             sincosf(yw, &syw, &cyw);
             yaw = atan2f(syw, cyw);
             if constexpr (PROFILE == ISAAC) {
+                if (SWARM_ABLATE & 16) continue;
                 walls_dg(g, x, y);
                 gate_walls<MISSION, ISAAC>(g, x, y);
-                robots_push(g, L, T, x, y);
-                resolve_collisions<MISSION>(g, L, T, x, y, true, qx, qy);
+                robots_push<W, C>(g, L, S, x, y);
+                resolve_collisions<MISSION, W, C>(g, L, S, x, y, true, qx, qy);
             } else {
                 walls_mc(g, x, y);
                 gate_walls<MISSION, STANDALONE>(g, x, y);
-                robots_push(g, L, T, x, y);
+                robots_push<W, C>(g, L, S, x, y);
             }
         }
 
@@ -913,7 +1100,7 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
         if constexpr (PROFILE == ISAAC) {
             ep_len += 1;
             tout = ep_len >= g.max_len;                                      // DG:1200-1209
-            if (tout && L.valid) {
+            if (tout && L.valid && L.wv == 0) {
                 float c5[5];
                 critic5(g, x, y, yaw, c5);
                 float* o = st.tcrit + q * 5;
@@ -930,7 +1117,7 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
                 if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
             }
             if ((reset_any >> s) & 1ull) {                                   // DG:1262 (all envs)
-                resolve_collisions<MISSION>(g, L, T, x, y, false, 0.0f, 0.0f);
+                resolve_collisions<MISSION, W, C>(g, L, S, x, y, false, 0.0f, 0.0f);
             }
             if (tout) {
                 gprev = ground_code<MISSION, PROFILE>(g, x, y);
@@ -956,11 +1143,11 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        observe<MISSION, PROFILE>(g, L, T, x, y, yaw, u_obs, tick, out.obs, cache);
+        observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache);
     }
 
-    // ---- store state and per-call outputs ----
-    if (L.valid) {
+    // ---- store state and per-call outputs (wave 0; all waves hold the same values) ----
+    if (L.valid && L.wv == 0) {
         st.x[q] = x;
         st.y[q] = y;
         st.yaw[q] = yaw;
@@ -988,13 +1175,15 @@ __global__ __launch_bounds__(64) void step_kernel(const Geom g, const DevState s
 // ---------------------------------------------------------------------------
 //  Reset kernel: _reset_idx(mask) + observations (DirectMARLEnv.reset)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE>
+template <int MISSION, int PROFILE, int NA>
 __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState st, const uint8_t* __restrict__ mask,
                                                    const DevOut out, const DevReplay rp, uint64_t tick) {
-    __shared__ Tile T;
-    const Lane L = make_lane(g);
-    const size_t q = L.valid ? (size_t)L.env * g.N + L.i : 0;
-    const size_t EN = (size_t)g.E * g.N;
+    constexpr int W = 1;
+    constexpr int C = NA > 0 ? NA : 0;
+    __shared__ Shared<W> S;
+    const Lane L = make_lane<NA, W>(g);
+    const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
+    const size_t EN = (size_t)g.E * L.N;
     float x = 0.0f, y = 0.0f, yaw = 0.0f;
     bool doit = false;
     if (L.valid) {
@@ -1011,11 +1200,11 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
         }
     }
     if constexpr (PROFILE == ISAAC) {
-        resolve_collisions<MISSION>(g, L, T, x, y, false, 0.0f, 0.0f);      // DG:1262 (all envs)
+        resolve_collisions<MISSION, W, C>(g, L, S, x, y, false, 0.0f, 0.0f);  // DG:1262 (all envs)
     }
     Agg agg;
-    const float* u_obs = rp.rab ? rp.rab + (size_t)(L.valid ? L.env : 0) * g.N * g.N + (size_t)L.i * g.N : nullptr;
-    observe<MISSION, PROFILE>(g, L, T, x, y, yaw, u_obs, tick, out.obs, agg);
+    const float* u_obs = rp.rab ? rp.rab + (size_t)(L.valid ? L.env : 0) * L.N * L.N + (size_t)L.i * L.N : nullptr;
+    observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, agg);
     if (L.valid) {
         st.x[q] = x;
         st.y[q] = y;
@@ -1044,22 +1233,32 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
     }
 }
 
-__global__ void critic_kernel(const Geom g, const float* __restrict__ x, const float* __restrict__ y,
-                              const float* __restrict__ yaw, float* __restrict__ out) {
-    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= (size_t)g.E * g.N) return;
-    critic5(g, x[q], y[q], yaw[q], out + q * 5);
-}
-
 // ---------------------------------------------------------------------------
-//  Host-side launchers (called by swarm_capi.cpp)
+//  Host-side launchers (instantiated once per mission by swarm_mission.hip)
 // ---------------------------------------------------------------------------
 template <int M, int P, bool D>
 static void launch_step_t(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
                           const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
     const int blocks = (g.E + g.apb - 1) / g.apb;
-    hipLaunchKernelGGL((step_kernel<M, P, D>), dim3(blocks), dim3(64), 0, stream, g, st, act, ovr, out, rp, tick, n_sub,
-                       reset_any);
+#define SWARM_LAUNCH_STEP(NA, W)                                                                                      \
+    hipLaunchKernelGGL((step_kernel<M, P, D, NA, W>), dim3(blocks), dim3(64 * W), 0, stream, g, st, act, ovr, out, rp, \
+                       tick, n_sub, reset_any)
+    if (g.N == 20) {
+        if (g.waves == 4)
+            SWARM_LAUNCH_STEP(20, 4);
+        else if (g.waves == 2)
+            SWARM_LAUNCH_STEP(20, 2);
+        else
+            SWARM_LAUNCH_STEP(20, 1);
+    } else {
+        if (g.waves == 4)
+            SWARM_LAUNCH_STEP(0, 4);
+        else if (g.waves == 2)
+            SWARM_LAUNCH_STEP(0, 2);
+        else
+            SWARM_LAUNCH_STEP(0, 1);
+    }
+#undef SWARM_LAUNCH_STEP
 }
 
 template <int M, int P>
@@ -1072,7 +1271,7 @@ static void launch_step_md(const Geom& g, const DevState& st, const void* act, c
 }
 
 template <int M>
-static void launch_step_m(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
+void launch_step_m(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
                           const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
     if (g.profile == ISAAC)
         launch_step_md<M, ISAAC>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
@@ -1080,43 +1279,15 @@ static void launch_step_m(const Geom& g, const DevState& st, const void* act, co
         launch_step_md<M, STANDALONE>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream);
 }
 
-void launch_step(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
-                 const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
-    switch (g.mission) {
-    case DIRGATE: launch_step_m<DIRGATE>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
-    case XOR: launch_step_m<XOR>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
-    case HOMING: launch_step_m<HOMING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
-    case FORAGING: launch_step_m<FORAGING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
-    default: launch_step_m<SHELTERING>(g, st, act, ovr, out, rp, tick, n_sub, reset_any, stream); break;
-    }
-}
-
 template <int M>
-static void launch_reset_m(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out,
+void launch_reset_m(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out,
                            const DevReplay& rp, uint64_t tick, hipStream_t stream) {
     const int blocks = (g.E + g.apb - 1) / g.apb;
     if (g.profile == ISAAC)
-        hipLaunchKernelGGL((reset_kernel<M, ISAAC>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp, tick);
+        hipLaunchKernelGGL((reset_kernel<M, ISAAC, 0>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp, tick);
     else
-        hipLaunchKernelGGL((reset_kernel<M, STANDALONE>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp,
+        hipLaunchKernelGGL((reset_kernel<M, STANDALONE, 0>), dim3(blocks), dim3(64), 0, stream, g, st, mask, out, rp,
                            tick);
-}
-
-void launch_reset(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out, const DevReplay& rp,
-                  uint64_t tick, hipStream_t stream) {
-    switch (g.mission) {
-    case DIRGATE: launch_reset_m<DIRGATE>(g, st, mask, out, rp, tick, stream); break;
-    case XOR: launch_reset_m<XOR>(g, st, mask, out, rp, tick, stream); break;
-    case HOMING: launch_reset_m<HOMING>(g, st, mask, out, rp, tick, stream); break;
-    case FORAGING: launch_reset_m<FORAGING>(g, st, mask, out, rp, tick, stream); break;
-    default: launch_reset_m<SHELTERING>(g, st, mask, out, rp, tick, stream); break;
-    }
-}
-
-void launch_critic(const Geom& g, const float* x, const float* y, const float* yaw, float* out, hipStream_t stream) {
-    const size_t n = (size_t)g.E * g.N;
-    const int blocks = (int)((n + 255) / 256);
-    hipLaunchKernelGGL(critic_kernel, dim3(blocks), dim3(256), 0, stream, g, x, y, yaw, out);
 }
 
 }  // namespace swarm
