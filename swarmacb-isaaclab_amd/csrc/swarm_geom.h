@@ -70,6 +70,7 @@ struct Geom {
     float r_robot, min_dist, r2, max_speed, wheelbase, dt;
     // squared-distance pre-filters: s >= x2_hi guarantees fl(sqrt(s)) >= x (x^2 (1 + 2^-20))
     float min_dist2_hi, rab_range2_hi;
+    float inv_prox_range, inv_unity;  // 1/0.1 rounded to float (= 10)
     float prox_range, rab_range, rab_loss, unity, light_thr, light_int, alpha, prox_thr;
     float pi_f, two_pi_f, half_pi_f, critic_radius;
 };

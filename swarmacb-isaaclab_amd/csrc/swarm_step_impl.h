@@ -36,6 +36,17 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
+// 1: compile-time neighbour chunks are held in registers and processed
+// predicated (fully unrolled); 0: candidate bitmask + ctz loop (smaller code).
+#ifndef SWARM_UNROLLED_CHUNKS
+#define SWARM_UNROLLED_CHUNKS 0
+#endif
+
+// Register budget: minimum resident waves per SIMD the compiler must allow.
+#ifndef SWARM_MIN_WAVES_PER_SIMD
+#define SWARM_MIN_WAVES_PER_SIMD 4
+#endif
+
 // Timing-only ablation switches (tools/ablate.sh builds variants with
 // -DSWARM_ABLATE=mask; results are then WRONG by design). 0 in every product build.
 #ifndef SWARM_ABLATE
@@ -82,6 +93,14 @@ __device__ __forceinline__ float u01_of5(const uint4& r, int w) {
     }
     return (float)v * (1.0f / 16777216.0f);
 }
+
+// Hardware reciprocal / square root (v_rcp_f32, v_sqrt_f32: ~1 ulp) for values
+// that only feed arithmetic or hit tests whose reading is continuous across the
+// test's boundary (a ray exactly at a segment end / at the 0.1 m range reads the
+// same either way). Threshold tests that decide a discrete outcome (contact
+// overlap, RAB range, line of sight) keep IEEE division / sqrt.
+__device__ __forceinline__ float frcp(float v) { return __builtin_amdgcn_rcpf(v); }
+__device__ __forceinline__ float fsqrt(float v) { return __builtin_amdgcn_sqrtf(v); }
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
@@ -178,37 +197,52 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
     if (SWARM_ABLATE & 4) return;
     if (L.wv == 0) S.xy[L.lane] = make_float2(x, y);
     sync_wg<W>();
+    float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
-    unsigned long long cand = 0;
+    auto pair_term = [&](int j, float dx, float dy) {
+        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        const float ov = g.min_dist - dist;
+        if (!(ov > 0.0f)) return;
+        const float inv = frcp(dist + 1e-8f);
+        const float nx = dx * inv, ny = dy * inv;
+        if (j > L.i) {  // row term of pair (i, j)
+            rx += ov * nx * 0.5f;
+            ry += ov * ny * 0.5f;
+        } else {        // column term of pair (j, i): n_ji = -n_ij
+            cx += ov * (-nx) * 0.5f;
+            cy += ov * (-ny) * 0.5f;
+        }
+    };
+    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
+        // compile-time chunk: the C neighbour positions stay in registers and the
+        // exact term runs predicated (skipped by the wave when no lane needs it)
+        float2 p[C];
 #pragma unroll
-    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
-        const int j = L.j0 + jj;
-        if (C == 0 && j >= L.j1) break;
-        if (C > 0 && j >= L.j1) continue;
-        const float2 p = S.xy[L.ab + j];
-        const float dx = x - p.x, dy = y - p.y;
-        const float s = dx * dx + dy * dy + 1e-8f;
-        if (j != L.i && s < g.min_dist2_hi) cand |= 1ull << j;
-    }
-    float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
-    {
+        for (int jj = 0; jj < C; ++jj) p[jj] = S.xy[L.ab + min(L.j0 + jj, L.N - 1)];
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) {
+            const int j = L.j0 + jj;
+            const float dx = x - p[jj].x, dy = y - p[jj].y;
+            const float s = dx * dx + dy * dy + 1e-8f;
+            if (j < L.j1 && j != L.i && s < g.min_dist2_hi) pair_term(j, dx, dy);
+        }
+    } else {
+        unsigned long long cand = 0;
+#pragma unroll
+        for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+            const int j = L.j0 + jj;
+            if (j >= L.j1) break;
+            const float2 p = S.xy[L.ab + j];
+            const float dx = x - p.x, dy = y - p.y;
+            const float s = dx * dx + dy * dy + 1e-8f;
+            if (j != L.i && s < g.min_dist2_hi) cand |= 1ull << j;
+        }
         while (cand) {
             const int j = __builtin_ctzll(cand);
             cand &= cand - 1ull;
             const float2 p = S.xy[L.ab + j];
-            const float dx = x - p.x, dy = y - p.y;
-            const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
-            const float ov = g.min_dist - dist;
-            if (!(ov > 0.0f)) continue;
-            const float nx = dx / (dist + 1e-8f), ny = dy / (dist + 1e-8f);
-            if (j > L.i) {  // row term of pair (i, j)
-                rx += ov * nx * 0.5f;
-                ry += ov * ny * 0.5f;
-            } else {        // column term of pair (j, i): n_ji = -n_ij
-                cx += ov * (-nx) * 0.5f;
-                cy += ov * (-ny) * 0.5f;
-            }
+            pair_term(j, x - p.x, y - p.y);
         }
     }
     if constexpr (W > 1) {
@@ -346,32 +380,40 @@ __device__ __forceinline__ void capsules(const Geom& g, float& x, float& y, bool
 }
 
 // DG:874-896 — pre pass, solver iterations, post pass.
-template <int MISSION, int W, int C>
-__device__ __forceinline__ void resolve_collisions(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y,
-                                                   bool has_prev, float qx, float qy) {
+template <int MISSION, int W, int C, bool APPLY>
+__device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y, float qx,
+                                      float qy) {
+    // Both contact sequences of the Isaac profile as one fully unrolled loop
+    // (straight-line code measured faster than a rolled loop here):
+    //  apply  (env.step, DG:829-836 then _resolve_collisions(prev_pos) DG:874-896):
+    //         walls, gate, {push, walls, internal(i == 0 || i == 5 ? prev : before), gate} i = 0..5, no push at i = 5
+    //  !apply (reset: _resolve_collisions() without prev_pos, DG:1262):
+    //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
+    constexpr bool apply = APPLY;
     walls_dg(g, x, y);
     if constexpr (INTERNAL) {
-        if (has_prev) anti_tunnel(g, x, y, qx, qy);
-        capsules(g, x, y, has_prev, qx, qy);
+        if (!apply) capsules(g, x, y, false, 0.0f, 0.0f);
     }
     gate_walls<MISSION, ISAAC>(g, x, y);
-    for (int it = 0; it < 4; ++it) {                     // collision_solver_iterations (DGC:127)
+    constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
+#pragma unroll
+    for (int it = 0; it <= K; ++it) {
         const float bx = x, by = y;
-        robots_push<W, C>(g, L, S, x, y);
+        if (it < K) robots_push<W, C>(g, L, S, x, y);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
-            anti_tunnel(g, x, y, bx, by);
-            capsules(g, x, y, true, bx, by);
+            const bool edge = apply ? (it == 0 || it == K) : (it == K);
+            if (edge && !apply) {
+                capsules(g, x, y, false, 0.0f, 0.0f);
+            } else {
+                const float px = edge ? qx : bx, py = edge ? qy : by;
+                anti_tunnel(g, x, y, px, py);
+                capsules(g, x, y, true, px, py);
+            }
         }
         gate_walls<MISSION, ISAAC>(g, x, y);
     }
-    walls_dg(g, x, y);
-    if constexpr (INTERNAL) {
-        if (has_prev) anti_tunnel(g, x, y, qx, qy);
-        capsules(g, x, y, has_prev, qx, qy);
-    }
-    gate_walls<MISSION, ISAAC>(g, x, y);
 }
 
 // ---------------------------------------------------------------------------
@@ -438,39 +480,53 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float den = rdx[k] * sy - rdy[k] * sx;
             const bool valid = fabsf(den) > 1e-8f;
             const float dd = den + 1e-12f;
-            const float t = (qx * sy - qy * sx) / dd;
-            const float u = (qx * rdy[k] - qy * rdx[k]) / dd;
+            const float inv = frcp(dd);
+            const float t = (qx * sy - qy * sx) * inv;
+            const float u = (qx * rdy[k] - qy * rdx[k]) * inv;
             const bool hit = valid && t >= 0.0f && t <= g.prox_range && u >= 0.0f && u <= 1.0f;
-            const float nr = hit ? 1.0f - t / g.prox_range : 0.0f;
+            const float nr = hit ? 1.0f - t * g.inv_prox_range : 0.0f;
             prox[k] = fmaxf(prox[k], nr);
         }
     }
     // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
-    unsigned long long cand = 0;
-#pragma unroll
-    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
-        const int j = L.j0 + jj;
-        if (C == 0 && j >= L.j1) break;
-        if (C > 0 && j >= L.j1) continue;
-        const float2 p = S.xy[L.ab + j];
-        const float dx = p.x - x, dy = p.y - y;
-        if (j != L.i && dx * dx + dy * dy <= 0.0200f) cand |= 1ull << j;
-    }
-    while (cand) {
-        const int j = __builtin_ctzll(cand);
-        cand &= cand - 1ull;
-        const float2 p = S.xy[L.ab + j];
-        const float dx = p.x - x, dy = p.y - y;
+    auto disc = [&](float dx, float dy) {
         const float dsq = dx * dx + dy * dy;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float proj = rdx[k] * dx + rdy[k] * dy;
             const float csq = dsq - proj * proj;
-            const float hc = sqrtf(fmaxf(g.r2 - csq, 0.0f));
+            const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
             const float hd = fmaxf(proj - hc, 0.0f);
             const bool hit = proj > 0.0f && csq <= g.r2 && hd <= g.prox_range;
-            const float rv = clampf(1.0f - hd / g.prox_range, 0.0f, 1.0f);
+            const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
+        }
+    };
+    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
+        float2 p[C];
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) p[jj] = S.xy[L.ab + min(L.j0 + jj, L.N - 1)];
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) {
+            const int j = L.j0 + jj;
+            const float dx = p[jj].x - x, dy = p[jj].y - y;
+            if (j < L.j1 && j != L.i && dx * dx + dy * dy <= 0.0200f) disc(dx, dy);
+        }
+    } else {
+        unsigned long long cand = 0;
+#pragma unroll
+        for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+            const int j = L.j0 + jj;
+            if (j >= L.j1) break;
+            const float2 p = S.xy[L.ab + j];
+            const float dx = p.x - x, dy = p.y - y;
+            if (j != L.i && dx * dx + dy * dy <= 0.0200f) cand |= 1ull << j;
+        }
+        while (cand) {
+            const int j = __builtin_ctzll(cand);
+            cand &= cand - 1ull;
+            const float2 p = S.xy[L.ab + j];
+            disc(p.x - x, p.y - y);
         }
     }
 }
@@ -499,8 +555,9 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
     }
     const float lx = g.light_x - x, ly = g.light_y - y;
     const float dist = sqrtf(lx * lx + ly * ly + 1e-6f);
-    const float base = g.light_int / (dist / g.unity);
-    const float nlx = lx / (dist + 1e-8f), nly = ly / (dist + 1e-8f);
+    const float base = g.light_int * frcp(dist * g.inv_unity);
+    const float il = frcp(dist + 1e-8f);
+    const float nlx = lx * il, nly = ly * il;
     float mx = 0.0f, sx = 0.0f, sy = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -526,45 +583,16 @@ template <int C>
 __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv, float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
                                             uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy) {
-    // in-range candidates from the squared distance (superset), exact test in the loop
-    unsigned long long cand = 0;
-#pragma unroll
-    for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
-        const int j = L.j0 + jj;
-        if (C == 0 && j >= L.j1) break;
-        if (C > 0 && j >= L.j1) continue;
-        const float2 p = xy[L.ab + j];
-        const float dx = p.x - x, dy = p.y - y;
-        const float s = dx * dx + dy * dy + 1e-8f;
-        if (j != L.i && s < g.rab_range2_hi) cand |= 1ull << j;
-    }
     const bool me_in = insv[L.lane] != 0;
     n = 0.0f;
     wx = 0.0f;
     wy = 0.0f;
     axx = 0.0f;
     ayy = 0.0f;
-    int blk = -1;
-    uint4 rb = make_uint4(0, 0, 0, 0);
-    while (cand) {
-        const int j = __builtin_ctzll(cand);
-        cand &= cand - 1ull;
-        float uu;
-        if (u_replay) {
-            uu = u_replay[j];
-        } else {
-            const int b = j / 5;
-            if (b != blk) {
-                blk = b;
-                rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
-            }
-            uu = u01_of5(rb, j - 5 * b);
-        }
-        if (!(uu >= g.rab_loss)) continue;
-        const float2 p = xy[L.ab + j];
-        const float dx = p.x - x, dy = p.y - y;
+    // one kept, in-range neighbour (exact distance test, LOS, bearing terms)
+    auto term = [&](int j, float dx, float dy) {
         const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
-        if (!(dist < g.rab_range)) continue;
+        if (!(dist < g.rab_range)) return;
         // line of sight (ES:462-501): arena faces can only block if an end point is
         // not strictly inside the convex arena; internal walls are always tested.
         const bool test_arena = !(me_in && insv[L.ab + j] != 0);
@@ -579,20 +607,92 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             const float u = (qx * rdy - qy * rdx) / dd;
             blocked |= fabsf(den) > 1e-8f && t > 1e-5f && t < dist - 1e-5f && u >= 0.0f && u <= 1.0f;
         }
-        if (blocked) continue;
+        if (blocked) return;
         n += 1.0f;
-        const float du = dist / g.unity;
-        const float inv = 1.0f / (du + 1e-8f);
+        const float du = dist * g.inv_unity;
+        const float inv = frcp(du + 1e-8f);
         const float bx = dx * cyw + dy * syw;
         const float by = -dx * syw + dy * cyw;
-        const float br = atan2f(by, bx);
-        float sb, cb;
-        sincosf(br, &sb, &cb);
+        // cos / sin of the bearing atan2(by, bx) (ES:433-438) taken from the
+        // vector itself (same values up to rounding, without atan2 + sincos)
+        const float hb2 = bx * bx + by * by;
+        float cb = 1.0f, sb = 0.0f;
+        if (hb2 > 0.0f) {
+            const float ih = frcp(fsqrt(hb2));
+            cb = bx * ih;
+            sb = by * ih;
+        }
         wx += inv * cb;
         wy += inv * sb;
-        const float aw = g.alpha / (1.0f + du);
+        const float aw = g.alpha * frcp(1.0f + du);
         axx += aw * cb;
         ayy += aw * sb;
+    };
+    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
+        // compile-time chunk: positions in registers; the Philox blocks of the
+        // chunk are drawn once per wave (only if some lane has a candidate)
+        float2 p[C];
+        bool cnd[C];
+        bool anyc = false;
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) {
+            const int j = L.j0 + jj;
+            p[jj] = xy[L.ab + min(j, L.N - 1)];
+            const float dx = p[jj].x - x, dy = p[jj].y - y;
+            const float s = dx * dx + dy * dy + 1e-8f;
+            cnd[jj] = j < L.j1 && j != L.i && s < g.rab_range2_hi;
+            anyc |= cnd[jj];
+        }
+        if (!__any(anyc)) return;
+        int blk = -1;
+        uint4 rb = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int jj = 0; jj < C; ++jj) {
+            const int j = L.j0 + jj;
+            float uu;
+            if (u_replay) {
+                uu = cnd[jj] ? u_replay[min(j, L.N - 1)] : 0.0f;
+            } else {
+                const int b = j / 5;   // wave-uniform
+                if (b != blk) {
+                    blk = b;
+                    rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
+                }
+                uu = u01_of5(rb, j - 5 * b);
+            }
+            if (cnd[jj] && uu >= g.rab_loss) term(j, p[jj].x - x, p[jj].y - y);
+        }
+    } else {
+        unsigned long long cand = 0;
+#pragma unroll
+        for (int jj = 0; jj < (C > 0 ? C : 64); ++jj) {
+            const int j = L.j0 + jj;
+            if (j >= L.j1) break;
+            const float2 q = xy[L.ab + j];
+            const float dx = q.x - x, dy = q.y - y;
+            const float s = dx * dx + dy * dy + 1e-8f;
+            if (j != L.i && s < g.rab_range2_hi) cand |= 1ull << j;
+        }
+        int blk = -1;
+        uint4 rb = make_uint4(0, 0, 0, 0);
+        while (cand) {
+            const int j = __builtin_ctzll(cand);
+            cand &= cand - 1ull;
+            float uu;
+            if (u_replay) {
+                uu = u_replay[j];
+            } else {
+                const int b = j / 5;
+                if (b != blk) {
+                    blk = b;
+                    rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
+                }
+                uu = u01_of5(rb, j - 5 * b);
+            }
+            if (!(uu >= g.rab_loss)) continue;
+            const float2 q = xy[L.ab + j];
+            term(j, q.x - x, q.y - y);
+        }
     }
 }
 
@@ -697,6 +797,21 @@ __device__ __forceinline__ void dispatch(const Geom& g, const Lane& L, int mod, 
     }
 }
 
+// ES:592-617 differential drive + DG:816-826 / MC:360-366 integration and yaw
+// wrap. (sy, cy) = sin/cos of the current yaw (carried from the observation
+// pass, which evaluates them anyway). The reference wraps with
+// atan2(sin(yw), cos(yw)): the identity on (-pi, pi) up to rounding, so the
+// wrap is done explicitly (pi_f > pi, so yw = +-pi_f already wraps, as atan2 does).
+__device__ __forceinline__ void integrate(const Geom& g, float lw, float rw, float& x, float& y, float& yaw, float sy,
+                                          float cy) {
+    const float v = 0.5f * (lw + rw);
+    const float om = (rw - lw) / g.wheelbase;
+    x += v * cy * g.dt;
+    y += v * sy * g.dt;
+    const float yw = yaw + om * g.dt;
+    yaw = yw >= g.pi_f ? yw - g.two_pi_f : (yw <= -g.pi_f ? yw + g.two_pi_f : yw);
+}
+
 // ---------------------------------------------------------------------------
 //  Critic state (ES:545-586 with DG's centre (0,0), radius 1.2, reference +Y)
 // ---------------------------------------------------------------------------
@@ -784,9 +899,9 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<W>& S, bool with_p
 // ---------------------------------------------------------------------------
 template <int MISSION, int PROFILE, int W, int C>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float yaw,
-                                        const float* u_replay, uint64_t tick, float* obs, Agg& agg) {
+                                        const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
+                                        float& cyw) {
     publish<W>(g, L, S, x, y);
-    float syw, cyw;
     sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
 #pragma unroll
@@ -838,11 +953,9 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>&
 // standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
 // proximity/light aggregates equal those of the previous observation (same pose).
 template <int W, int C>
-__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float yaw,
-                                         const float* u_replay, uint64_t tick, float& ax, float& ay) {
+__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float syw,
+                                         float cyw, const float* u_replay, uint64_t tick, float& ax, float& ay) {
     publish<W>(g, L, S, x, y);
-    float syw, cyw;
-    sincosf(yaw, &syw, &cyw);
     float n, wx, wy;
     rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax, ay);
     combine<W, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
@@ -979,7 +1092,7 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {
 }
 
 template <int MISSION, int PROFILE, bool DISCRETE, int NA, int W>
-__global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
+__global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
                                                       const float* __restrict__ ovr, const DevOut out,
                                                       const DevReplay rp, uint64_t tick0, int n_sub,
                                                       uint64_t reset_any) {
@@ -1032,6 +1145,8 @@ __global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevSta
     }
     float rew_acc = 0.0f;
     bool trunc_acc = false;
+    float syaw, cyaw;                 // sin / cos of the current yaw, carried between substeps
+    sincosf(yaw, &syaw, &cyaw);
 
     for (int s = 0; s < n_sub; ++s) {
         const uint64_t tick = tick0 + (uint64_t)s;
@@ -1044,7 +1159,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevSta
         if constexpr (PROFILE == STANDALONE) {
             const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
                                         : nullptr;
-            rab_only<W, C>(g, L, S, x, y, yaw, u_d, tick, cache.ax, cache.ay);
+            rab_only<W, C>(g, L, S, x, y, syaw, cyaw, u_d, tick, cache.ax, cache.ay);
             if constexpr (DISCRETE) {
                 dispatch(g, L, mod, cache, 0.0f, 0.0f, fsm, ts, lw, rw);   // previous = zeros (MC:744-747)
             } else {
@@ -1069,35 +1184,16 @@ __global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevSta
         wr = rw;
 
         // ------------------------------ physics ------------------------------
-        const int nd = PROFILE == ISAAC ? g.decimation : 1;
-        for (int d = 0; d < nd; ++d) {
-            const float qx = x, qy = y;
-            const float v = 0.5f * (lw + rw);
-            const float om = (rw - lw) / g.wheelbase;
-            float sy, cy;
-            sincosf(yaw, &sy, &cy);
-            x += v * cy * g.dt;
-            y += v * sy * g.dt;
-            const float yw = yaw + om * g.dt;
-            float syw, cyw;
-            sincosf(yw, &syw, &cyw);
-            yaw = atan2f(syw, cyw);
-            if constexpr (PROFILE == ISAAC) {
-                if (SWARM_ABLATE & 16) continue;
-                walls_dg(g, x, y);
-                gate_walls<MISSION, ISAAC>(g, x, y);
-                robots_push<W, C>(g, L, S, x, y);
-                resolve_collisions<MISSION, W, C>(g, L, S, x, y, true, qx, qy);
-            } else {
-                walls_mc(g, x, y);
-                gate_walls<MISSION, STANDALONE>(g, x, y);
-                robots_push<W, C>(g, L, S, x, y);
-            }
-        }
-
-        // ------------------------- dones / rewards / reset -------------------------
         bool tout;
         if constexpr (PROFILE == ISAAC) {
+            // decimation x {integrate, contacts}, then dones / rewards / auto-reset,
+            // then (if any env of the batch reset) the solver again on all envs.
+            for (int d = 0; d < g.decimation; ++d) {
+                const float qx = x, qy = y;
+                if (d > 0) sincosf(yaw, &syaw, &cyaw);
+                integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
+                if (!(SWARM_ABLATE & 16)) solve<MISSION, W, C, true>(g, L, S, x, y, qx, qy);
+            }
             ep_len += 1;
             tout = ep_len >= g.max_len;                                      // DG:1200-1209
             if (tout && L.valid && L.wv == 0) {
@@ -1116,15 +1212,18 @@ __global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevSta
                 ep_rew = 0.0f;
                 if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
             }
-            if ((reset_any >> s) & 1ull) {                                   // DG:1262 (all envs)
-                resolve_collisions<MISSION, W, C>(g, L, S, x, y, false, 0.0f, 0.0f);
-            }
+            if ((reset_any >> s) & 1ull)                                     // DG:1262 (all envs)
+                solve<MISSION, W, C, false>(g, L, S, x, y, 0.0f, 0.0f);
             if (tout) {
                 gprev = ground_code<MISSION, PROFILE>(g, x, y);
                 fsm = 0u;
                 if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
             }
         } else {
+            integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
+            walls_mc(g, x, y);
+            gate_walls<MISSION, STANDALONE>(g, x, y);
+            robots_push<W, C>(g, L, S, x, y);
             const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, ep_len + 1 >= g.max_len);
             ep_rew += r;
             rew_acc += r;
@@ -1143,7 +1242,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(const Geom g, const DevSta
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache);
+        observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw);
     }
 
     // ---- store state and per-call outputs (wave 0; all waves hold the same values) ----
@@ -1200,11 +1299,12 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
         }
     }
     if constexpr (PROFILE == ISAAC) {
-        resolve_collisions<MISSION, W, C>(g, L, S, x, y, false, 0.0f, 0.0f);  // DG:1262 (all envs)
+        solve<MISSION, W, C, false>(g, L, S, x, y, 0.0f, 0.0f);  // DG:1262 (all envs)
     }
     Agg agg;
+    float syaw, cyaw;
     const float* u_obs = rp.rab ? rp.rab + (size_t)(L.valid ? L.env : 0) * L.N * L.N + (size_t)L.i * L.N : nullptr;
-    observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, agg);
+    observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, agg, syaw, cyaw);
     if (L.valid) {
         st.x[q] = x;
         st.y[q] = y;

@@ -7,12 +7,15 @@ cd "$(dirname "$0")/.."
 MASKS=${MASKS:-"0 1 2 3 4 8 16 31"}
 OUT=build/ablate
 if [ "$1" = build ]; then
+  # variants differ only in the Homing translation unit: reuse the other objects
+  make -s -j8 -C swarmacb-isaaclab_amd/csrc || exit 1
   mkdir -p $OUT
   for m in $MASKS; do
-    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -DSWARM_ABLATE=$m -shared \
-      -o $OUT/lib_$m.so swarmacb-isaaclab_amd/csrc/swarm_kernels.hip -x hip swarmacb-isaaclab_amd/csrc/swarm_capi.cpp &
+    rm -rf $OUT/obj_$m && cp -rp build/obj $OUT/obj_$m && rm -f $OUT/obj_$m/swarm_mission_2.o
+    make -s -C swarmacb-isaaclab_amd/csrc OBJDIR=$PWD/$OUT/obj_$m OUT=$PWD/$OUT/lib_$m.so EXTRA=-DSWARM_ABLATE=$m &
   done
   wait
+  rm -rf $OUT/obj_*
   ls -la $OUT
   exit 0
 fi
