@@ -37,6 +37,7 @@ import torch  # noqa: E402
 METRIC = "agent-steps/sec (20 e-pucks × num_envs) SwarmACB-Homing-v0 at 1/2/4/8 MI355X"
 ALGO_BYTES_PER_AGENT_STEP = 129.0   # read x,y,yaw+action 20 B, write x,y,yaw+obs 108 B, ~1 B counters
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9   # MI355X_MICROARCH.md: 256 CUs, 4 SIMD32 each, 2.4 GHz max clock
 N_AGENTS = 20
 
 
@@ -82,17 +83,19 @@ def cpu_baseline(budget_s: float, envs: int) -> dict | None:
                       f"({el:.1f} s, 1 thread, host CPU)"}
 
 
-def load_traffic(envs: int, sub: int) -> float | None:
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if it matches."""
+def load_pmc(envs: int, sub: int) -> dict:
+    """Per-launch HBM bytes and VALU instruction count of the step kernel from the
+    committed rocprofv3 PMC record (profiles/pmc_traffic.json, tools/pmc.sh), if it
+    was taken on this workload."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return {}
     if d.get("envs") != envs or d.get("substeps") != sub:
-        return None
-    return d.get("hbm_bytes_per_launch")
+        return {}
+    return d
 
 
 def main():
@@ -155,7 +158,16 @@ def main():
     if rank == 0:
         bytes_per_launch = ALGO_BYTES_PER_AGENT_STEP * E * N_AGENTS * dp
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        traffic = load_traffic(E, dp)
+        pmc = load_pmc(E, dp)
+        traffic = pmc.get("hbm_bytes_per_launch")
+        valu = None
+        if pmc.get("valu_insts_per_launch"):
+            # VALU issue roof: 256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz (a wave64 VALU op = 64 lane-ops)
+            lane_ops = pmc["valu_insts_per_launch"] * 64.0
+            peak = VALU_PEAK_LANE_OPS
+            valu = {"achieved": lane_ops / avg_kernel_s / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s",
+                    "frac": lane_ops / avg_kernel_s / peak,
+                    "valu_insts_per_launch": pmc["valu_insts_per_launch"]}
         line = {
             "metric": METRIC,
             "value": value,
@@ -187,7 +199,9 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "step_kernel<HOMING,ISAAC,continuous>",
+                "traffic_per_agent_step": (traffic / (E * N_AGENTS * dp)) if traffic else None,
+                "valu": valu,
+                "kernel": "step_kernel<HOMING,ISAAC,continuous,N=20,W>",
                 "kernel_avg_us": avg_kernel_s * 1e6,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },

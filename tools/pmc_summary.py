@@ -68,12 +68,35 @@ def main(root: str):
         for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
             if k in c:
                 res[k.lower() + "_frac"] = c[k] / wc
+    if "SQ_INSTS_VALU" in c:
+        res["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
     out["derived"] = res
     out["counters"] = c
     print(json.dumps(out, indent=1, sort_keys=True))
     with open(os.path.join(root, "summary.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+    return out
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc")
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--traffic-json", default=None, help="write the bench's traffic record here")
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--substeps", type=int, default=5)
+    ap.add_argument("--wg-waves", type=int, default=0)
+    a = ap.parse_args()
+    o = main(a.root)
+    if a.traffic_json:
+        d = o["derived"]
+        rec = {"envs": a.envs, "substeps": a.substeps, "wg_waves": a.wg_waves,
+               "hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
+               "fetch_bytes_raw": d.get("fetch_bytes_raw"), "write_bytes": d.get("write_bytes"),
+               "valu_insts_per_launch": d.get("valu_insts_per_launch"),
+               "kernel_resources": o.get("kernel_resources"),
+               "method": "rocprofv3 --pmc, one counter group per pass (FETCH_SIZE, WRITE_SIZE, SQ_*), "
+                         "averaged over step_kernel dispatches; FETCH_SIZE x2 (gfx950 half-count), KiB -> B"}
+        with open(a.traffic_json, "w") as f:
+            json.dump(rec, f, indent=1, sort_keys=True)
