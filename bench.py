@@ -114,9 +114,11 @@ def main():
     torch.cuda.set_device(dev)
 
     from SwarmACB_isaac.engine import SwarmEngine
+    from SwarmACB_isaac.shard import EnvShard, max_over_ranks
 
     E, dp = args.envs, args.decision_period
-    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, rank * E, args.seed, dev,
+    shard = EnvShard.weak(E, rank, world)     # weak scaling: E envs per GPU, keyed by global env id
+    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, shard.env_offset, args.seed, dev,
                       wg_waves=args.wg_waves or None)
     obs, rew, tr = eng.reset()
     out = (obs, rew, tr)
@@ -148,10 +150,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
     total_agent_steps = world * E * N_AGENTS * steps
     value = total_agent_steps / elapsed
 
