@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--decision-period", type=int, default=5)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo")
     ap.add_argument("--wg-waves", type=int, default=0, help="waves per workgroup (1, 2, 4; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
     return ap.parse_args()
@@ -104,14 +105,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU; (rank % visible devices) only matters when rehearsing
+    # several ranks on one device (with --dist-backend gloo: RCCL refuses that)
+    local = local % max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from SwarmACB_isaac.engine import SwarmEngine
     from SwarmACB_isaac.shard import EnvShard, max_over_ranks
