@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--decision-period", type=int, default=5)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo")
-    ap.add_argument("--wg-waves", type=int, default=0, help="waves per workgroup (1, 2, 4; 0 = library default)")
+    ap.add_argument("--layout", type=int, default=0,
+                    help="kernel work layout (1/2/4 waves per 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
     return ap.parse_args()
 
@@ -125,7 +126,7 @@ def main():
     E, dp = args.envs, args.decision_period
     shard = EnvShard.weak(E, rank, world)     # weak scaling: E envs per GPU, keyed by global env id
     eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, shard.env_offset, args.seed, dev,
-                      wg_waves=args.wg_waves or None)
+                      layout=args.layout or None)
     obs, rew, tr = eng.reset()
     out = (obs, rew, tr)
 
@@ -193,7 +194,7 @@ def main():
                 "num_agents": N_AGENTS,
                 "global_envs": world * E,
                 "decision_period": dp,
-                "wg_waves": args.wg_waves or "default",
+                "layout": args.layout or "default",
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,
             },

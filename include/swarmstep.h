@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SWARM_ABI_VERSION 1
+#define SWARM_ABI_VERSION 2
 #define SWARM_MAX_AGENTS 64
 #define SWARM_MAX_SUBSTEPS 64
 
@@ -72,7 +72,9 @@ typedef struct {
     int32_t discrete_actions;     /* 1: action = behaviour-module id (int32); 0: wheels (float2) */
     int32_t max_episode_length;   /* steps; isaac ceil(episode_length_s/(dt*decimation)) */
     int32_t decimation;           /* isaac physics substeps per env.step (DGC:97) */
-    int32_t wg_waves;             /* waves cooperating on one workgroup's arenas: 1, 2, 4 (0 = auto) */
+    int32_t layout;               /* work layout: 0 = auto, 1/2/4 = that many waves share 3 arenas
+                                     (one lane per robot), 103 = one arena per wave, 3 lanes
+                                     per robot (needs num_agents <= 21) */
     int64_t env_offset;           /* global index of local env 0 (multi-GPU sharding) */
     uint64_t seed;                /* Philox key for all in-kernel randomness */
 } swarm_params_t;

@@ -12,7 +12,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SWARMSTEP_LIB", os.path.join(HERE, "libswarmstep.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_AGENTS = 64
 MAX_SUBSTEPS = 64
 
@@ -25,7 +25,7 @@ class SwarmParams(C.Structure):
         ("abi_version", C.c_int32), ("mission", C.c_int32), ("profile", C.c_int32),
         ("num_envs", C.c_int32), ("num_agents", C.c_int32), ("obs_dim", C.c_int32),
         ("discrete_actions", C.c_int32), ("max_episode_length", C.c_int32), ("decimation", C.c_int32),
-        ("wg_waves", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
+        ("layout", C.c_int32), ("env_offset", C.c_int64), ("seed", C.c_uint64),
     ]
 
 

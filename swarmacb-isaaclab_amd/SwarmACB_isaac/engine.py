@@ -59,7 +59,7 @@ class SwarmEngine:
 
     def __init__(self, mission: str, profile: str = "isaac", num_envs: int = 1, num_agents: int = 20,
                  obs_dim: int = 24, discrete: bool = False, max_episode_length: int = 1200,
-                 decimation: int = 1, env_offset: int = 0, seed: int = 0, device="cuda:0", wg_waves: int | None = None):
+                 decimation: int = 1, env_offset: int = 0, seed: int = 0, device="cuda:0", layout: int | None = None):
         self.lib = _native.load()
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -71,7 +71,7 @@ class SwarmEngine:
         self.params = _native.SwarmParams(
             _native.ABI_VERSION, _native.MISSIONS[mission], _native.PROFILES[profile], self.E, self.N,
             self.obs_dim, int(self.discrete), self.max_episode_length, int(decimation),
-            int(wg_waves if wg_waves is not None else os.environ.get("SWARM_WG_WAVES", 0)),
+            int(layout if layout is not None else os.environ.get("SWARM_LAYOUT", 0)),
             int(env_offset), int(seed) & 0xFFFFFFFFFFFFFFFF)
         h = C.c_void_p()
         _native.check(self.lib.swarm_create(C.byref(self.params), C.byref(h)), "swarm_create")

@@ -80,7 +80,7 @@ void build_geom(const swarm_params_t& p, Geom& g) {
     g.max_len = p.max_episode_length;
     g.decimation = p.decimation > 0 ? p.decimation : 1;
     g.apb = 64 / p.num_agents;
-    g.waves = p.wg_waves > 0 ? p.wg_waves : 4;
+    g.layout = p.layout > 0 ? p.layout : (3 * p.num_agents <= 64 ? 103 : 4);
     g.seed_lo = (uint32_t)p.seed;
     g.seed_hi = (uint32_t)(p.seed >> 32);
     g.env_off_lo = (uint32_t)p.env_offset;
@@ -302,7 +302,8 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     if (p->num_envs < 1 || p->num_agents < 1 || p->num_agents > SWARM_MAX_AGENTS) return SWARM_ERR_ARG;
     if (p->obs_dim != 24 && p->obs_dim != 4) return SWARM_ERR_ARG;
     if (p->max_episode_length < 1 || p->decimation < 0 || p->env_offset < 0) return SWARM_ERR_ARG;
-    if (p->wg_waves != 0 && p->wg_waves != 1 && p->wg_waves != 2 && p->wg_waves != 4) return SWARM_ERR_ARG;
+    if (p->layout != 0 && p->layout != 1 && p->layout != 2 && p->layout != 4 && p->layout != 103) return SWARM_ERR_ARG;
+    if (p->layout == 103 && 3 * p->num_agents > 64) return SWARM_ERR_ARG;
     swarm_handle_t* h = new (std::nothrow) swarm_handle_t();
     if (!h) return SWARM_ERR_ARG;
     h->p = *p;

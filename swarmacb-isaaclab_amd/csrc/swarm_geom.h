@@ -26,7 +26,7 @@ struct Geom {
     int32_t mission, profile, N, E;
     int32_t obs_dim, discrete, max_len, decimation;
     int32_t apb;            // arenas per 64-lane wave (= 64 / N)
-    int32_t waves;          // cooperating waves per workgroup (1, 2 or 4)
+    int32_t layout;         // workgroup layout LY (swarm_step_impl.h): 1, 2, 4 waves or 103
     int32_t nseg, nint;     // raycast segments (arena 12 + internal), internal walls
     int32_t has_light;
     uint32_t seed_lo, seed_hi;

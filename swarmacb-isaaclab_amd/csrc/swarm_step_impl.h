@@ -80,8 +80,30 @@ __device__ __forceinline__ uint4 rng4(const Geom& g, uint32_t genv, uint32_t rob
 // torch-style float uniform from 24 random bits: [0, 1)
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
 
-// Five independent 24-bit uniforms from one Philox block (120 of its 128 bits):
-// the packet-loss draws of neighbours j = 5*blk .. 5*blk+4.
+// Packet-loss uniforms of one part's neighbour chunk. The Philox block of
+// (robot, part p, sub-block) is fixed by the chunk index jj = j - j0, so the
+// draws do not depend on how envs are sharded. A 6- or 7-neighbour chunk (3
+// parts x N = 20) takes seven 18-bit uniforms from ONE block (126 bits);
+// otherwise blocks of five 24-bit uniforms (120 bits each).
+template <int C>
+struct ChunkRng {
+    static constexpr bool K18 = (C == 6 || C == 7);
+    __device__ static __forceinline__ uint32_t block(int p, int jj) { return (uint32_t)(16 * p + (K18 ? 0 : jj / 5)); }
+    __device__ static __forceinline__ bool fresh(int jj) { return K18 ? jj == 0 : jj % 5 == 0; }
+};
+
+__device__ __forceinline__ float u01_of7(const uint4& r, int w) {
+    const unsigned long long lo = (unsigned long long)r.x | ((unsigned long long)r.y << 32);
+    const unsigned long long hi = (unsigned long long)r.z | ((unsigned long long)r.w << 32);
+    const int o = 18 * w;
+    unsigned long long v;
+    if (o + 18 <= 64) v = lo >> o;
+    else if (o >= 64) v = hi >> (o - 64);
+    else v = (lo >> o) | (hi << (64 - o));
+    return (float)(uint32_t)(v & 0x3FFFFull) * (1.0f / 262144.0f);
+}
+
+// Five independent 24-bit uniforms from one Philox block (120 of its 128 bits).
 __device__ __forceinline__ float u01_of5(const uint4& r, int w) {
     uint32_t v;
     switch (w) {
@@ -128,27 +150,40 @@ __device__ __forceinline__ uint32_t fsm_put(Fsm m, int sh) {
 // ---------------------------------------------------------------------------
 //  Per-lane context
 // ---------------------------------------------------------------------------
+// Workgroup layout LY (compile time): a robot's O(N) work is split over
+// P = waves x lanes "parts" that hold bit-identical copies of its state.
+//   LY = 1, 2, 4 : LY waves, one lane per robot; each wave holds ⌊64/N⌋ whole
+//                  arenas, part p = wave index (wave-uniform)
+//   LY = 103     : one wave, 3 adjacent lanes per robot (robot-major: lane =
+//                  a*3N + 3i + p), one arena per wave for N <= 21; partials are
+//                  exchanged inside the wave, no cross-wave barrier at all
+constexpr int ly_waves(int LY) { return LY >= 100 ? 1 : LY; }
+constexpr int ly_lanes(int LY) { return LY >= 100 ? LY - 100 : 1; }
+constexpr int ly_parts(int LY) { return ly_waves(LY) * ly_lanes(LY); }
+
 struct Lane {
     int N;                    // robots per arena (a compile-time constant for the N = 20 specialisation)
-    int wv;                   // wave index inside the workgroup (wave-uniform, in an SGPR)
-    int j0, j1;               // this wave's neighbour chunk [j0, j1)
-    int lane, a, i, env, ab;  // ab = LDS base of this lane's arena
+    int p;                    // part index of this thread (0 .. P-1): owns neighbour chunk [j0, j1)
+    int j0, j1;
+    int tid;                  // thread index in the workgroup (partial-slot index)
+    int pbase, pstride;       // thread of part k = pbase + k * pstride
+    int a, i, env, ab, r;     // arena in the wave, robot, env; ab = tile base of the arena, r = ab + i
     bool valid;
     uint32_t genv;
-    unsigned long long amask;  // ballot bits of this lane's arena
+    unsigned long long amask;  // ballot bits of this arena's part-0 lanes
 };
 
 // LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
-// broadcast within an arena) and W x 4 float4 partial slots per lane.
+// broadcast within an arena) and 4 float4 partial slots per thread.
 // Slot use: 0 contact-solver sums, 0-1 proximity maxima, 2-3 range-and-bearing sums.
-template <int W>
+template <int LY>
 struct Shared {
     float2 xy[64];
     int ins[64];
-    float4 red[W > 1 ? W : 1][4][64];
+    float4 red[4][64 * ly_waves(LY)];
 };
 
-template <int W>
+template <int LY>
 __device__ __forceinline__ void sync_wg() {
     __syncthreads();
 }
@@ -192,11 +227,11 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 
 // DG:1080-1112 / MC:555-571 — Jacobi half-overlap push over pairs i<j.
 // Each wave sums its neighbour chunk; the W partial sums are added in wave order.
-template <int W, int C>
-__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y) {
+template <int LY, int C>
+__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
     if (SWARM_ABLATE & 4) return;
-    if (L.wv == 0) S.xy[L.lane] = make_float2(x, y);
-    sync_wg<W>();
+    if (L.p == 0) S.xy[L.r] = make_float2(x, y);
+    sync_wg<LY>();
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
@@ -245,13 +280,13 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
             pair_term(j, x - p.x, y - p.y);
         }
     }
-    if constexpr (W > 1) {
-        S.red[L.wv][0][L.lane] = make_float4(rx, ry, cx, cy);
-        sync_wg<W>();
-        float4 a = S.red[0][0][L.lane];
+    if constexpr (ly_parts(LY) > 1) {
+        S.red[0][L.tid] = make_float4(rx, ry, cx, cy);
+        sync_wg<LY>();
+        float4 a = S.red[0][L.pbase];
 #pragma unroll
-        for (int k = 1; k < W; ++k) {
-            const float4 b = S.red[k][0][L.lane];
+        for (int k = 1; k < ly_parts(LY); ++k) {
+            const float4 b = S.red[0][L.pbase + k * L.pstride];
             a.x += b.x;
             a.y += b.y;
             a.z += b.z;
@@ -262,7 +297,7 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
         cx = a.z;
         cy = a.w;
     } else {
-        sync_wg<W>();
+        sync_wg<LY>();
     }
     x = (x + rx) - cx;
     y = (y + ry) - cy;
@@ -380,8 +415,8 @@ __device__ __forceinline__ void capsules(const Geom& g, float& x, float& y, bool
 }
 
 // DG:874-896 — pre pass, solver iterations, post pass.
-template <int MISSION, int W, int C, bool APPLY>
-__device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<W>& S, float& x, float& y, float qx,
+template <int MISSION, int LY, int C, bool APPLY>
+__device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y, float qx,
                                       float qy) {
     // Both contact sequences of the Isaac profile as one fully unrolled loop
     // (straight-line code measured faster than a rolled loop here):
@@ -400,7 +435,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<W>& S
 #pragma unroll
     for (int it = 0; it <= K; ++it) {
         const float bx = x, by = y;
-        if (it < K) robots_push<W, C>(g, L, S, x, y);
+        if (it < K) robots_push<LY, C>(g, L, S, x, y);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
@@ -454,13 +489,13 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // ES:85-142, 184-293: per-ray readings (max over segments and robot discs).
 // Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
-template <int W, int C>
-__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const Shared<W>& S, float x, float y,
+template <int LY, int C>
+__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const Shared<LY>& S, float x, float y,
                                                   const float rdx[8], const float rdy[8], float prox[8]) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length
-    for (int s = L.wv; s < g.nseg; s += W) {
+    for (int s = L.p; s < g.nseg; s += ly_parts(LY)) {
         bool near;
         if (s < 12) {
             const float sd = (x - g.face_px[s]) * g.face_nx[s] + (y - g.face_py[s]) * g.face_ny[s];
@@ -583,7 +618,7 @@ template <int C>
 __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv, float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
                                             uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy) {
-    const bool me_in = insv[L.lane] != 0;
+    const bool me_in = insv[L.r] != 0;
     n = 0.0f;
     wx = 0.0f;
     wy = 0.0f;
@@ -644,7 +679,6 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             anyc |= cnd[jj];
         }
         if (!__any(anyc)) return;
-        int blk = -1;
         uint4 rb = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int jj = 0; jj < C; ++jj) {
@@ -653,12 +687,9 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             if (u_replay) {
                 uu = cnd[jj] ? u_replay[min(j, L.N - 1)] : 0.0f;
             } else {
-                const int b = j / 5;   // wave-uniform
-                if (b != blk) {
-                    blk = b;
-                    rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
-                }
-                uu = u01_of5(rb, j - 5 * b);
+                if (ChunkRng<C>::fresh(jj))
+                    rb = rng4(g, L.genv, (uint32_t)L.i, ChunkRng<C>::block(L.p, jj), purpose, tick);
+                uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
             }
             if (cnd[jj] && uu >= g.rab_loss) term(j, p[jj].x - x, p[jj].y - y);
         }
@@ -673,21 +704,22 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             const float s = dx * dx + dy * dy + 1e-8f;
             if (j != L.i && s < g.rab_range2_hi) cand |= 1ull << j;
         }
-        int blk = -1;
+        uint32_t blk = 0xFFFFFFFFu;
         uint4 rb = make_uint4(0, 0, 0, 0);
         while (cand) {
             const int j = __builtin_ctzll(cand);
             cand &= cand - 1ull;
+            const int jj = j - L.j0;
             float uu;
             if (u_replay) {
                 uu = u_replay[j];
             } else {
-                const int b = j / 5;
+                const uint32_t b = ChunkRng<C>::block(L.p, jj);
                 if (b != blk) {
                     blk = b;
-                    rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)blk, purpose, tick);
+                    rb = rng4(g, L.genv, (uint32_t)L.i, blk, purpose, tick);
                 }
-                uu = u01_of5(rb, j - 5 * b);
+                uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
             }
             if (!(uu >= g.rab_loss)) continue;
             const float2 q = xy[L.ab + j];
@@ -831,38 +863,40 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
 // Publishes positions + "strictly inside the arena" flags (LOS shortcut).
-template <int W>
-__device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<W>& S, float x, float y) {
+template <int LY>
+__device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y) {
     bool ins = true;
 #pragma unroll
     for (int k = 0; k < 12; ++k)
         ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
-    if (L.wv == 0) {
-        S.xy[L.lane] = make_float2(x, y);
-        S.ins[L.lane] = ins ? 1 : 0;
+    if (L.p == 0) {
+        S.xy[L.r] = make_float2(x, y);
+        S.ins[L.r] = ins ? 1 : 0;
     }
-    sync_wg<W>();
+    sync_wg<LY>();
 }
 
 // Range-and-bearing sums over all neighbours: this wave's chunk + the other
 // waves' partials (slots 2-3), added in wave order. Must follow publish().
 // With `with_prox`, also max-combines the proximity readings (slots 0-1).
-template <int W, int C>
-__device__ __forceinline__ void combine(const Lane& L, Shared<W>& S, bool with_prox, float prox[8], float& n,
+template <int LY, int C>
+__device__ __forceinline__ void combine(const Lane& L, Shared<LY>& S, bool with_prox, float prox[8], float& n,
                                         float& wx, float& wy, float& axx, float& ayy) {
-    if constexpr (W > 1) {
+    if constexpr (ly_parts(LY) > 1) {
+        constexpr int P = ly_parts(LY);
         if (with_prox) {
-            S.red[L.wv][0][L.lane] = make_float4(prox[0], prox[1], prox[2], prox[3]);
-            S.red[L.wv][1][L.lane] = make_float4(prox[4], prox[5], prox[6], prox[7]);
+            S.red[0][L.tid] = make_float4(prox[0], prox[1], prox[2], prox[3]);
+            S.red[1][L.tid] = make_float4(prox[4], prox[5], prox[6], prox[7]);
         }
-        S.red[L.wv][2][L.lane] = make_float4(n, wx, wy, axx);
-        S.red[L.wv][3][L.lane].x = ayy;
-        sync_wg<W>();
+        S.red[2][L.tid] = make_float4(n, wx, wy, axx);
+        S.red[3][L.tid].x = ayy;
+        sync_wg<LY>();
         if (with_prox) {
 #pragma unroll
-            for (int k = 0; k < W; ++k) {
-                if (k == L.wv) continue;
-                const float4 a = S.red[k][0][L.lane], b = S.red[k][1][L.lane];
+            for (int k = 0; k < P; ++k) {
+                if (k == L.p) continue;
+                const int o = L.pbase + k * L.pstride;
+                const float4 a = S.red[0][o], b = S.red[1][o];
                 prox[0] = fmaxf(prox[0], a.x);
                 prox[1] = fmaxf(prox[1], a.y);
                 prox[2] = fmaxf(prox[2], a.z);
@@ -873,16 +907,17 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<W>& S, bool with_p
                 prox[7] = fmaxf(prox[7], b.w);
             }
         }
-        float4 s = S.red[0][2][L.lane];
-        float sa = S.red[0][3][L.lane].x;
+        float4 s = S.red[2][L.pbase];
+        float sa = S.red[3][L.pbase].x;
 #pragma unroll
-        for (int k = 1; k < W; ++k) {
-            const float4 b = S.red[k][2][L.lane];
+        for (int k = 1; k < P; ++k) {
+            const int o = L.pbase + k * L.pstride;
+            const float4 b = S.red[2][o];
             s.x += b.x;
             s.y += b.y;
             s.z += b.z;
             s.w += b.w;
-            sa += S.red[k][3][L.lane].x;
+            sa += S.red[3][o].x;
         }
         n = s.x;
         wx = s.y;
@@ -890,18 +925,18 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<W>& S, bool with_p
         axx = s.w;
         ayy = sa;
     } else {
-        sync_wg<W>();
+        sync_wg<LY>();
     }
 }
 
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE, int W, int C>
-__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float yaw,
+template <int MISSION, int PROFILE, int LY, int C>
+__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw) {
-    publish<W>(g, L, S, x, y);
+    publish<LY>(g, L, S, x, y);
     sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
 #pragma unroll
@@ -914,11 +949,11 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>&
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<W, C>(g, L, S, x, y, rdx, rdy, prox);
+        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox);
     }
     if (!(SWARM_ABLATE & 1))
         rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy);
-    combine<W, C>(L, S, true, prox, n, wx, wy, axx, ayy);
+    combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     proximity_aggregate(g, prox, agg.pv, agg.pa);
     light(g, x, y, cyw, syw, lt, agg.lv, agg.la);
     rab_finish(g, n, wx, wy, zt, r4);
@@ -929,10 +964,10 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>&
         float* o = obs + ((size_t)L.env * L.N + L.i) * g.obs_dim;
         if (g.obs_dim == 24) {
             float4* o4 = reinterpret_cast<float4*>(o);
-            // chunk c of the 24-D row is stored by wave c % W
+            // chunk c of the 24-D row is stored by part c % P
 #pragma unroll
             for (int c = 0; c < 6; ++c) {
-                if (c % W != L.wv) continue;
+                if (c % ly_parts(LY) != L.p) continue;
                 float4 v;
                 switch (c) {
                 case 0: v = make_float4(prox[0], prox[1], prox[2], prox[3]); break;
@@ -944,7 +979,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>&
                 }
                 o4[c] = v;
             }
-        } else if (L.wv == 0) {
+        } else if (L.p == 0) {
             *reinterpret_cast<float4*>(o) = make_float4(gv, gv, gv, zt);
         }
     }
@@ -952,13 +987,13 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<W>&
 
 // standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
 // proximity/light aggregates equal those of the previous observation (same pose).
-template <int W, int C>
-__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<W>& S, float x, float y, float syw,
+template <int LY, int C>
+__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float syw,
                                          float cyw, const float* u_replay, uint64_t tick, float& ax, float& ay) {
-    publish<W>(g, L, S, x, y);
+    publish<LY>(g, L, S, x, y);
     float n, wx, wy;
     rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax, ay);
-    combine<W, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
+    combine<LY, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
 }
 
 // ---------------------------------------------------------------------------
@@ -1069,36 +1104,58 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 // ---------------------------------------------------------------------------
 // NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
 // every neighbour loop has a compile-time trip count and is fully unrolled.
-template <int NA, int W>
+template <int NA, int LY>
 __device__ __forceinline__ Lane make_lane(const Geom& g) {
+    constexpr int KL = ly_lanes(LY), P = ly_parts(LY);
     Lane L;
     L.N = NA > 0 ? NA : g.N;
-    const int apb = NA > 0 ? 64 / (NA > 0 ? NA : 1) : g.apb;
-    L.lane = threadIdx.x & 63;
-    L.wv = W > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
-    const int chunk = (L.N + W - 1) / W;
-    L.j0 = L.wv * chunk;
+    const int lane = threadIdx.x & 63;
+    L.tid = threadIdx.x;
+    int apb;                                      // arenas per wave
+    if constexpr (KL > 1) {
+        apb = 64 / (KL * L.N);
+        const int a = lane / (KL * L.N), rem = lane - a * (KL * L.N);
+        L.a = a;
+        L.i = rem / KL;
+        L.p = rem - L.i * KL;
+        L.pbase = L.tid - L.p;
+        L.pstride = 1;
+    } else {
+        apb = NA > 0 ? 64 / (NA > 0 ? NA : 1) : g.apb;
+        L.a = lane / L.N;
+        L.i = lane - L.a * L.N;
+        L.p = P > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+        L.pbase = lane;
+        L.pstride = 64;
+    }
+    const int chunk = (L.N + P - 1) / P;
+    L.j0 = L.p * chunk;
     L.j1 = min(L.N, L.j0 + chunk);
-    L.a = L.lane / L.N;
-    L.i = L.lane - L.a * L.N;
     L.env = blockIdx.x * apb + L.a;
     L.valid = (L.a < apb) && (L.env < g.E);
     L.ab = (L.a < apb ? L.a : 0) * L.N;
+    // lanes beyond the last whole arena own no robot: park their tile writes in
+    // slot 63, which no arena uses unless all 64 lanes hold robots
+    L.r = (L.a < apb) ? L.ab + L.i : 63;
     const uint64_t goff = ((uint64_t)g.env_off_hi << 32) | g.env_off_lo;
     L.genv = (uint32_t)(goff + (uint64_t)(L.env < g.E ? L.env : 0));
-    const unsigned long long m = L.N >= 64 ? ~0ull : ((1ull << L.N) - 1ull);
-    L.amask = (L.a < apb) ? (m << L.ab) : 0ull;
+    // ballot mask: the part-0 lanes of this lane's arena
+    unsigned long long m = 0;
+    if (L.a < apb) {
+        for (int q = 0; q < L.N; ++q) m |= 1ull << (L.a * KL * L.N + q * KL);
+    }
+    L.amask = m;
     return L;
 }
 
-template <int MISSION, int PROFILE, bool DISCRETE, int NA, int W>
-__global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
+template <int MISSION, int PROFILE, bool DISCRETE, int NA, int LY>
+__global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
                                                       const float* __restrict__ ovr, const DevOut out,
                                                       const DevReplay rp, uint64_t tick0, int n_sub,
                                                       uint64_t reset_any) {
-    constexpr int C = NA > 0 ? (NA + W - 1) / W : 0;   // neighbour chunk per wave (0 = runtime)
-    __shared__ Shared<W> S;
-    const Lane L = make_lane<NA, W>(g);
+    constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
+    __shared__ Shared<LY> S;
+    const Lane L = make_lane<NA, LY>(g);
     const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
     const size_t EN = (size_t)g.E * L.N;
 
@@ -1159,7 +1216,7 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
         if constexpr (PROFILE == STANDALONE) {
             const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
                                         : nullptr;
-            rab_only<W, C>(g, L, S, x, y, syaw, cyaw, u_d, tick, cache.ax, cache.ay);
+            rab_only<LY, C>(g, L, S, x, y, syaw, cyaw, u_d, tick, cache.ax, cache.ay);
             if constexpr (DISCRETE) {
                 dispatch(g, L, mod, cache, 0.0f, 0.0f, fsm, ts, lw, rw);   // previous = zeros (MC:744-747)
             } else {
@@ -1192,11 +1249,11 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
                 const float qx = x, qy = y;
                 if (d > 0) sincosf(yaw, &syaw, &cyaw);
                 integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
-                if (!(SWARM_ABLATE & 16)) solve<MISSION, W, C, true>(g, L, S, x, y, qx, qy);
+                if (!(SWARM_ABLATE & 16)) solve<MISSION, LY, C, true>(g, L, S, x, y, qx, qy);
             }
             ep_len += 1;
             tout = ep_len >= g.max_len;                                      // DG:1200-1209
-            if (tout && L.valid && L.wv == 0) {
+            if (tout && L.valid && L.p == 0) {
                 float c5[5];
                 critic5(g, x, y, yaw, c5);
                 float* o = st.tcrit + q * 5;
@@ -1213,7 +1270,7 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
                 if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
             }
             if ((reset_any >> s) & 1ull)                                     // DG:1262 (all envs)
-                solve<MISSION, W, C, false>(g, L, S, x, y, 0.0f, 0.0f);
+                solve<MISSION, LY, C, false>(g, L, S, x, y, 0.0f, 0.0f);
             if (tout) {
                 gprev = ground_code<MISSION, PROFILE>(g, x, y);
                 fsm = 0u;
@@ -1223,7 +1280,7 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
             integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
             walls_mc(g, x, y);
             gate_walls<MISSION, STANDALONE>(g, x, y);
-            robots_push<W, C>(g, L, S, x, y);
+            robots_push<LY, C>(g, L, S, x, y);
             const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, ep_len + 1 >= g.max_len);
             ep_rew += r;
             rew_acc += r;
@@ -1242,11 +1299,11 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw);
+        observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw);
     }
 
     // ---- store state and per-call outputs (wave 0; all waves hold the same values) ----
-    if (L.valid && L.wv == 0) {
+    if (L.valid && L.p == 0) {
         st.x[q] = x;
         st.y[q] = y;
         st.yaw[q] = yaw;
@@ -1277,10 +1334,10 @@ __global__ __launch_bounds__(64 * W, SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
 template <int MISSION, int PROFILE, int NA>
 __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState st, const uint8_t* __restrict__ mask,
                                                    const DevOut out, const DevReplay rp, uint64_t tick) {
-    constexpr int W = 1;
+    constexpr int LY = 1;
     constexpr int C = NA > 0 ? NA : 0;
-    __shared__ Shared<W> S;
-    const Lane L = make_lane<NA, W>(g);
+    __shared__ Shared<LY> S;
+    const Lane L = make_lane<NA, LY>(g);
     const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
     const size_t EN = (size_t)g.E * L.N;
     float x = 0.0f, y = 0.0f, yaw = 0.0f;
@@ -1299,12 +1356,12 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
         }
     }
     if constexpr (PROFILE == ISAAC) {
-        solve<MISSION, W, C, false>(g, L, S, x, y, 0.0f, 0.0f);  // DG:1262 (all envs)
+        solve<MISSION, LY, C, false>(g, L, S, x, y, 0.0f, 0.0f);  // DG:1262 (all envs)
     }
     Agg agg;
     float syaw, cyaw;
     const float* u_obs = rp.rab ? rp.rab + (size_t)(L.valid ? L.env : 0) * L.N * L.N + (size_t)L.i * L.N : nullptr;
-    observe<MISSION, PROFILE, W, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, agg, syaw, cyaw);
+    observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, agg, syaw, cyaw);
     if (L.valid) {
         st.x[q] = x;
         st.y[q] = y;
@@ -1339,21 +1396,29 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
 template <int M, int P, bool D>
 static void launch_step_t(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
                           const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
+#define SWARM_LAUNCH_STEP(NA, LY)                                                                                   \
+    hipLaunchKernelGGL((step_kernel<M, P, D, NA, LY>), dim3(blocks), dim3(64 * ly_waves(LY)), 0, stream, g, st, act, \
+                       ovr, out, rp, tick, n_sub, reset_any)
+    if (g.layout == 103) {   // one arena per wave, 3 lanes per robot (N <= 21, checked by swarm_create)
+        const int blocks = g.E;
+        if (g.N == 20)
+            SWARM_LAUNCH_STEP(20, 103);
+        else
+            SWARM_LAUNCH_STEP(0, 103);
+        return;
+    }
     const int blocks = (g.E + g.apb - 1) / g.apb;
-#define SWARM_LAUNCH_STEP(NA, W)                                                                                      \
-    hipLaunchKernelGGL((step_kernel<M, P, D, NA, W>), dim3(blocks), dim3(64 * W), 0, stream, g, st, act, ovr, out, rp, \
-                       tick, n_sub, reset_any)
     if (g.N == 20) {
-        if (g.waves == 4)
+        if (g.layout == 4)
             SWARM_LAUNCH_STEP(20, 4);
-        else if (g.waves == 2)
+        else if (g.layout == 2)
             SWARM_LAUNCH_STEP(20, 2);
         else
             SWARM_LAUNCH_STEP(20, 1);
     } else {
-        if (g.waves == 4)
+        if (g.layout == 4)
             SWARM_LAUNCH_STEP(0, 4);
-        else if (g.waves == 2)
+        else if (g.layout == 2)
             SWARM_LAUNCH_STEP(0, 2);
         else
             SWARM_LAUNCH_STEP(0, 1);

@@ -35,15 +35,16 @@ def test_library_exports_every_declared_symbol():
 
 
 def _params(**kw):
-    p = dict(abi_version=1, mission=2, profile=0, num_envs=4, num_agents=20, obs_dim=24, discrete_actions=0,
-             max_episode_length=1200, decimation=1, reserved0=0, env_offset=0, seed=0)
+    p = dict(abi_version=2, mission=2, profile=0, num_envs=4, num_agents=20, obs_dim=24, discrete_actions=0,
+             max_episode_length=1200, decimation=1, layout=0, env_offset=0, seed=0)
     p.update(kw)
     return _native.SwarmParams(**p)
 
 
-@pytest.mark.parametrize("bad", [dict(abi_version=2), dict(mission=9), dict(profile=3), dict(num_envs=0),
+@pytest.mark.parametrize("bad", [dict(abi_version=1), dict(mission=9), dict(profile=3), dict(num_envs=0),
                                  dict(num_agents=65), dict(num_agents=0), dict(obs_dim=7),
-                                 dict(max_episode_length=0), dict(env_offset=-1)])
+                                 dict(max_episode_length=0), dict(env_offset=-1), dict(layout=3),
+                                 dict(layout=103, num_agents=22)])
 def test_create_rejects_bad_params(bad):
     lib = _native.load()
     h = C.c_void_p()

@@ -18,12 +18,17 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
-def _engine(fx, device, seed=0):
+# kernel work layouts (include/swarmstep.h swarm_params_t.layout): 0 = library default
+# (103: one arena per wave, 3 lanes per robot), 4 = four waves share 3 arenas, 1 = one lane per robot
+LAYOUTS = [0, 4, 1]
+
+
+def _engine(fx, device, seed=0, layout=0):
     from SwarmACB_isaac.engine import SwarmEngine
 
     env, meta = O.fixture_env(fx)
     eng = SwarmEngine(meta["mission"], meta["profile"], env.E, env.N, env.obs_dim, meta["discrete"],
-                      env.cfg.max_len, 1, 0, seed, device)
+                      env.cfg.max_len, 1, 0, seed, device, layout=layout)
     eng.reset()
     return eng, env, meta
 
@@ -65,10 +70,11 @@ def _gpu_step(eng, fx, t, meta, device):
     return got
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("name", parity.fixture_ids())
-def test_gpu_matches_reference_golden(name, gpu_device):
+def test_gpu_matches_reference_golden(name, layout, gpu_device):
     fx = parity.load(name)
-    eng, _, meta = _engine(fx, gpu_device)
+    eng, _, meta = _engine(fx, gpu_device, layout=layout)
     failures = []
     for t in range(fx["obs"].shape[0]):
         got = _gpu_step(eng, fx, t, meta, gpu_device)
@@ -116,9 +122,10 @@ def _random_state(rng, E, N, mission):
     return s
 
 
+@pytest.mark.parametrize("layout", [0, 4])
 @pytest.mark.parametrize("mission", ["dgt", "xor", "homing", "foraging", "sheltering"])
 @pytest.mark.parametrize("profile,discrete", [("isaac", False), ("isaac", True), ("standalone", True)])
-def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
+def test_gpu_random_states_vs_oracle(mission, profile, discrete, layout, gpu_device):
     from SwarmACB_isaac.engine import SwarmEngine
 
     rng = np.random.default_rng(zlib.crc32(f"{mission}/{profile}/{discrete}".encode()))
@@ -150,7 +157,7 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
         ovr[:, 0] = [0.16, 0.12]
     obs_o, rew_o, tr_o = ora.step(acts, ovr, draws)
 
-    eng = SwarmEngine(mission, profile, E, N, obs_dim, discrete, max_len, 1, 0, 0, gpu_device)
+    eng = SwarmEngine(mission, profile, E, N, obs_dim, discrete, max_len, 1, 0, 0, gpu_device, layout=layout)
     eng.reset()
     eng.load_state(s)
     for k, v in s.items():
@@ -195,10 +202,11 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, gpu_device):
 #  Philox path: determinism, sharding invariance, decision fusion, statistics
 # --------------------------------------------------------------------------
 
-def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed=7, max_len=23, total=None):
+def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed=7, max_len=23, total=None,
+         layout=0):
     from SwarmACB_isaac.engine import SwarmEngine
 
-    eng = SwarmEngine(mission, "isaac", E, 20, 24, discrete, max_len, 1, offset, seed, device)
+    eng = SwarmEngine(mission, "isaac", E, 20, 24, discrete, max_len, 1, offset, seed, device, layout=layout)
     eng.reset()
     g = torch.Generator(device="cpu").manual_seed(1)
     outs = []
@@ -215,12 +223,13 @@ def _run(device, E, offset, steps, n_sub, mission="homing", discrete=False, seed
     return outs, st
 
 
+@pytest.mark.parametrize("layout", LAYOUTS)
 @pytest.mark.parametrize("discrete", [False, True])
-def test_sharding_invariance_bitwise(discrete, gpu_device):
+def test_sharding_invariance_bitwise(discrete, layout, gpu_device):
     """Envs split over two engines (env_offset) reproduce one engine bit for bit."""
-    full, st_full = _run(gpu_device, 6, 0, 30, 1, discrete=discrete, total=6)
-    lo, st_lo = _run(gpu_device, 3, 0, 30, 1, discrete=discrete, total=6)
-    hi, st_hi = _run(gpu_device, 3, 3, 30, 1, discrete=discrete, total=6)
+    full, st_full = _run(gpu_device, 6, 0, 30, 1, discrete=discrete, total=6, layout=layout)
+    lo, st_lo = _run(gpu_device, 3, 0, 30, 1, discrete=discrete, total=6, layout=layout)
+    hi, st_hi = _run(gpu_device, 3, 3, 30, 1, discrete=discrete, total=6, layout=layout)
     for (of, rf, tf), (ol, rl, tl), (oh, rh, th) in zip(full, lo, hi):
         assert torch.equal(of[:3], ol) and torch.equal(of[3:], oh)
         assert torch.equal(rf, torch.cat([rl, rh])) and torch.equal(tf, torch.cat([tl, th]))
@@ -260,10 +269,11 @@ def test_decision_fusion_equals_single_steps(gpu_device):
     np.testing.assert_array_equal(s1["pos"], s2["pos"])
 
 
-def test_determinism_and_seed_dependence(gpu_device):
-    a, _ = _run(gpu_device, 8, 0, 12, 1, seed=11)
-    b, _ = _run(gpu_device, 8, 0, 12, 1, seed=11)
-    c, _ = _run(gpu_device, 8, 0, 12, 1, seed=12)
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_determinism_and_seed_dependence(layout, gpu_device):
+    a, _ = _run(gpu_device, 8, 0, 12, 1, seed=11, layout=layout)
+    b, _ = _run(gpu_device, 8, 0, 12, 1, seed=11, layout=layout)
+    c, _ = _run(gpu_device, 8, 0, 12, 1, seed=12, layout=layout)
     assert all(torch.equal(x[0], y[0]) for x, y in zip(a, b))
     assert not all(torch.equal(x[0], y[0]) for x, y in zip(a, c))
 

@@ -86,12 +86,12 @@ if __name__ == "__main__":
     ap.add_argument("--traffic-json", default=None, help="write the bench's traffic record here")
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--substeps", type=int, default=5)
-    ap.add_argument("--wg-waves", type=int, default=0)
+    ap.add_argument("--layout", type=int, default=0)
     a = ap.parse_args()
     o = main(a.root)
     if a.traffic_json:
         d = o["derived"]
-        rec = {"envs": a.envs, "substeps": a.substeps, "wg_waves": a.wg_waves,
+        rec = {"envs": a.envs, "substeps": a.substeps, "layout": a.layout,
                "hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
                "fetch_bytes_raw": d.get("fetch_bytes_raw"), "write_bytes": d.get("write_bytes"),
                "valu_insts_per_launch": d.get("valu_insts_per_launch"),

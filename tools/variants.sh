@@ -29,7 +29,7 @@ if [ "$1" = pmc ]; then
       tag=$(echo $pass | cut -c1-12 | tr ' ' _)
       SWARMSTEP_LIB=$PWD/$lib timeout -k 10 300 rocprofv3 --kernel-include-regex step_kernel --pmc $pass \
         -d gpurun_out/vpmc/$name/$tag -o run --output-format csv -- python3 bench.py --cpu-seconds 0 --steps 100 --warmup 10 \
-        --wg-waves ${WAVES:-4} > gpurun_out/vpmc_$name.log 2>&1 || { echo "pmc $name failed"; tail -5 gpurun_out/vpmc_$name.log; exit 3; }
+        --layout ${WAVES:-4} > gpurun_out/vpmc_$name.log 2>&1 || { echo "pmc $name failed"; tail -5 gpurun_out/vpmc_$name.log; exit 3; }
     done
   done
   python3 tools/pmc_table.py gpurun_out/vpmc
@@ -38,7 +38,7 @@ fi
 for lib in $OUT/lib_*.so; do
   name=$(basename $lib .so); name=${name#lib_}
   for w in ${WAVES:-4}; do
-    SWARMSTEP_LIB=$PWD/$lib timeout -k 10 120 python3 bench.py --cpu-seconds 0 --steps 600 --wg-waves $w ${BENCH_ARGS:-} > gpurun_out/var_${name}_$w.log 2>&1 || { echo "$name W=$w failed"; tail -5 gpurun_out/var_${name}_$w.log; exit 3; }
+    SWARMSTEP_LIB=$PWD/$lib timeout -k 10 120 python3 bench.py --cpu-seconds 0 --steps 600 --layout $w ${BENCH_ARGS:-} > gpurun_out/var_${name}_$w.log 2>&1 || { echo "$name W=$w failed"; tail -5 gpurun_out/var_${name}_$w.log; exit 3; }
     python3 -c "import json; d=json.loads(open('gpurun_out/var_${name}_$w.log').read().strip().splitlines()[-1]); print('$name W=$w', 'value %.4g' % d['value'], 'kernel_us %.1f' % d['roofline']['kernel_avg_us'])"
   done
 done
