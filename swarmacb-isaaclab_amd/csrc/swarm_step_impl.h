@@ -579,9 +579,12 @@ __device__ __forceinline__ void proximity_aggregate(const Geom& g, const float p
 }
 
 // ES:299-356
+template <int MISSION>
 __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw, float syw, float lt[8], float& lv,
                                       float& la) {
-    if (!g.has_light) {
+    // Homing and XOR have no light (HMC:18, XOC:18; MC:144): readings are zero (DG:353-362)
+    constexpr bool HAS_LIGHT = !(MISSION == HOMING || MISSION == XOR);
+    if (!HAS_LIGHT) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) lt[k] = 0.0f;
         lv = 0.0f;
@@ -955,13 +958,13 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
         rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     proximity_aggregate(g, prox, agg.pv, agg.pa);
-    light(g, x, y, cyw, syw, lt, agg.lv, agg.la);
+    light<MISSION>(g, x, y, cyw, syw, lt, agg.lv, agg.la);
     rab_finish(g, n, wx, wy, zt, r4);
     agg.ax = axx;
     agg.ay = ayy;
     if (L.valid && obs) {
         const float gv = 0.5f * (float)ground_code<MISSION, PROFILE>(g, x, y);
-        float* o = obs + ((size_t)L.env * L.N + L.i) * g.obs_dim;
+        float* o = obs + ((uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i) * (uint32_t)g.obs_dim;
         if (g.obs_dim == 24) {
             float4* o4 = reinterpret_cast<float4*>(o);
             // chunk c of the 24-D row is stored by part c % P
@@ -1148,16 +1151,19 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {
     return L;
 }
 
-template <int MISSION, int PROFILE, bool DISCRETE, int NA, int LY>
-__global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void step_kernel(const Geom g, const DevState st, const void* __restrict__ actions,
-                                                      const float* __restrict__ ovr, const DevOut out,
-                                                      const DevReplay rp, uint64_t tick0, int n_sub,
-                                                      uint64_t reset_any) {
+// REPLAY = false is the production kernel: every replay pointer is a compile-time
+// null, so the replay-only paths (parity tests) cost it no registers or code.
+template <int MISSION, int PROFILE, bool DISCRETE, int NA, int LY, bool REPLAY>
+__global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
+    const Geom g, const DevState st, const void* __restrict__ actions, const float* __restrict__ ovr,
+    const DevOut out, const DevReplay rp_in, uint64_t tick0, int n_sub, uint64_t reset_any) {
+    const DevReplay rp = REPLAY ? rp_in : DevReplay{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
     const Lane L = make_lane<NA, LY>(g);
-    const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
-    const size_t EN = (size_t)g.E * L.N;
+    // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
+    const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
+    const uint32_t EN = (uint32_t)g.E * (uint32_t)L.N;
 
     // ---- load state (invalid lanes keep harmless values) ----
     float x = 0.0f, y = 0.0f, yaw = 0.0f, wl = 0.0f, wr = 0.0f;
@@ -1209,7 +1215,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         const uint64_t tick = tick0 + (uint64_t)s;
         const size_t NN = (size_t)L.N * L.N;
         const float* u_obs = rp.rab ? rp.rab + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
-        TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, EN, q, tick};
+        TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, (size_t)EN, (size_t)q, tick};
 
         // ------------------------------ actions ------------------------------
         float lw, rw;
@@ -1256,7 +1262,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             if (tout && L.valid && L.p == 0) {
                 float c5[5];
                 critic5(g, x, y, yaw, c5);
-                float* o = st.tcrit + q * 5;
+                float* o = st.tcrit + (size_t)q * 5;
 #pragma unroll
                 for (int k = 0; k < 5; ++k) o[k] = c5[k];
             }
@@ -1396,9 +1402,16 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState 
 template <int M, int P, bool D>
 static void launch_step_t(const Geom& g, const DevState& st, const void* act, const float* ovr, const DevOut& out,
                           const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream) {
-#define SWARM_LAUNCH_STEP(NA, LY)                                                                                   \
-    hipLaunchKernelGGL((step_kernel<M, P, D, NA, LY>), dim3(blocks), dim3(64 * ly_waves(LY)), 0, stream, g, st, act, \
-                       ovr, out, rp, tick, n_sub, reset_any)
+    const bool replay = rp.rab || rp.rab_d || rp.turns || rp.spawn || rp.spawn_yaw;
+#define SWARM_LAUNCH_STEP(NA, LY)                                                                                    \
+    do {                                                                                                              \
+        if (replay)                                                                                                   \
+            hipLaunchKernelGGL((step_kernel<M, P, D, NA, LY, true>), dim3(blocks), dim3(64 * ly_waves(LY)), 0, stream, \
+                               g, st, act, ovr, out, rp, tick, n_sub, reset_any);                                     \
+        else                                                                                                          \
+            hipLaunchKernelGGL((step_kernel<M, P, D, NA, LY, false>), dim3(blocks), dim3(64 * ly_waves(LY)), 0,       \
+                               stream, g, st, act, ovr, out, rp, tick, n_sub, reset_any);                             \
+    } while (0)
     if (g.layout == 103) {   // one arena per wave, 3 lanes per robot (N <= 21, checked by swarm_create)
         const int blocks = g.E;
         if (g.N == 20)
@@ -1411,15 +1424,11 @@ static void launch_step_t(const Geom& g, const DevState& st, const void* act, co
     if (g.N == 20) {
         if (g.layout == 4)
             SWARM_LAUNCH_STEP(20, 4);
-        else if (g.layout == 2)
-            SWARM_LAUNCH_STEP(20, 2);
         else
             SWARM_LAUNCH_STEP(20, 1);
     } else {
         if (g.layout == 4)
             SWARM_LAUNCH_STEP(0, 4);
-        else if (g.layout == 2)
-            SWARM_LAUNCH_STEP(0, 2);
         else
             SWARM_LAUNCH_STEP(0, 1);
     }

@@ -8,9 +8,10 @@ import re
 s = open('/tmp/cs.s').read()
 res = open('/tmp/cs_res.txt').read()
 for name in re.findall(r'^(_ZN5swarm11step_kernelI\w+):', s, re.M):
-    if 'Lb0ELi20E' not in name or 'ILi2ELi0E' not in name and 'ILi0ELi0E' not in name: continue
+    if 'Lb0ELi20E' not in name: continue
+    if not re.search(r'step_kernelILi\dELi0E', name): continue
     start = s.index(name + ':'); end = s.index('.Lfunc_end', start)
     n = sum(1 for l in s[start:end].split('\n') if l.startswith('\t') and not l.startswith('\t.') and not l.startswith('\t;'))
-    m = re.search(re.escape(name) + r'.*?VGPRs: (\d+).*?SGPRs Spill: (\d+).*?VGPRs Spill: (\d+)', res, re.S)
-    print(name[23:45], 'insts', n, 'vgpr/sgpr-spill/vgpr-spill', m.groups() if m else None)
+    m = re.search(re.escape(name) + r'.*?VGPRs: (\d+).*?ScratchSize \[bytes/lane\]: (\d+).*?SGPRs Spill: (\d+).*?VGPRs Spill: (\d+)', res, re.S)
+    print(name[23:50], 'insts', n, 'vgpr/scratch/sgpr-spill/vgpr-spill', m.groups() if m else None)
 PY
