@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -16,13 +17,17 @@
 
 #include "../../include/swarmstep.h"
 #include "swarm_geom.h"
+#include "swarm_geom_build.h"
+
+namespace swarm {
+#include "swarm_geom_tables.inc"
+}  // namespace swarm
 #include "swarm_launch.h"
 
 using namespace swarm;
 
 namespace {
 
-constexpr double PI = 3.14159265358979323846;
 thread_local int32_t g_last_hip = 0;
 
 // Histogram of episode lengths stored relative to a global offset: all envs
@@ -67,187 +72,6 @@ struct swarm_handle {
 };
 
 namespace {
-
-void build_geom(const swarm_params_t& p, Geom& g) {
-    std::memset(&g, 0, sizeof(g));
-    const bool mc = p.profile == SWARM_PROFILE_STANDALONE;
-    g.mission = p.mission;
-    g.profile = p.profile;
-    g.N = p.num_agents;
-    g.E = p.num_envs;
-    g.obs_dim = p.obs_dim;
-    g.discrete = p.discrete_actions;
-    g.max_len = p.max_episode_length;
-    g.decimation = p.decimation > 0 ? p.decimation : 1;
-    g.apb = 64 / p.num_agents;
-    g.layout = p.layout > 0 ? p.layout : (3 * p.num_agents <= 64 ? 103 : 4);
-    g.seed_lo = (uint32_t)p.seed;
-    g.seed_hi = (uint32_t)(p.seed >> 32);
-    g.env_off_lo = (uint32_t)p.env_offset;
-    g.env_off_hi = (uint32_t)((uint64_t)p.env_offset >> 32);
-
-    // arena: regular dodecagon of area 4.91 m^2 (DGC:32-36, DG:615-628)
-    const int n = 12;
-    const double R = std::sqrt(2 * 4.91 / (n * std::sin(2 * PI / n)));
-    double vx[12], vy[12];
-    for (int i = 0; i < n; ++i) {
-        const double a = 2 * PI * i / n + PI / n;
-        vx[i] = R * std::cos(a);
-        vy[i] = R * std::sin(a);
-    }
-    const double ni = R * std::cos(PI / n);
-    for (int i = 0; i < n; ++i) {
-        const double ax = vx[i], ay = vy[i], bx = vx[(i + 1) % n], by = vy[(i + 1) % n];
-        g.seg_ax[i] = (float)ax;
-        g.seg_ay[i] = (float)ay;
-        g.seg_sx[i] = (float)bx - (float)ax;  // torch: float32 tensor subtraction (ES:212)
-        g.seg_sy[i] = (float)by - (float)ay;
-        const double mx = 0.5 * (ax + bx), my = 0.5 * (ay + by);          // DG:858-868
-        const double nrm = std::sqrt(mx * mx + my * my) + 1e-12;
-        g.face_nx[i] = (float)(-mx / nrm);
-        g.face_ny[i] = (float)(-my / nrm);
-        g.face_px[i] = (float)mx;
-        g.face_py[i] = (float)my;
-        const double a1 = 2 * PI * i / n + PI / n;                          // MC:536-544
-        const double a2 = 2 * PI * ((i + 1) % n) / n + PI / n;
-        const double mid = (a1 + a2) / 2.0;
-        g.mcf_nx[i] = (float)(-std::cos(mid));
-        g.mcf_ny[i] = (float)(-std::sin(mid));
-        g.mcf_px[i] = (float)(ni * std::cos(mid));
-        g.mcf_py[i] = (float)(ni * std::sin(mid));
-    }
-    const double r = 0.035;
-    g.wall_clear_dg = (float)(r + 0.5 * 0.01 + 1e-4);                      // DG:1050-1054
-    g.wall_clear_mc = (float)r;                                             // MC:533
-
-    // mission zones (DG:649-656, DGC:163-167; SH:24-27 / MC:322-329)
-    const double corr_south = ni - 1.06, gate_south = corr_south - 0.33;
-    const double corr_hw = 0.25, gate_hw = 0.225;
-    double sh_l = -0.25, sh_r = 0.25, sh_b = -0.15, sh_t = 0.15;
-    if (mc) {  // MC goes through float32 tensors and .item()
-        sh_l = (double)(0.0f - 0.50f / 2.0f);
-        sh_r = (double)(0.0f + 0.50f / 2.0f);
-        sh_b = (double)(0.0f - 0.30f / 2.0f);
-        sh_t = (double)(0.0f + 0.30f / 2.0f);
-    }
-    // internal walls (DG:630-645 gate side walls, SH:29-35 shelter walls)
-    double iseg[3][4];
-    int nint = 0;
-    if (p.mission == SWARM_MISSION_DIRGATE) {
-        const double wl = 0.50;
-        const double s[2][4] = {{-corr_hw, gate_south, -corr_hw, gate_south + wl},
-                                {corr_hw, gate_south, corr_hw, gate_south + wl}};
-        std::memcpy(iseg, s, sizeof(s));
-        nint = 2;
-    } else if (p.mission == SWARM_MISSION_SHELTERING) {
-        const double s[3][4] = {{sh_l, sh_b, sh_l, sh_t}, {sh_r, sh_b, sh_r, sh_t}, {sh_l, sh_t, sh_r, sh_t}};
-        std::memcpy(iseg, s, sizeof(s));
-        nint = 3;
-    }
-    g.nint = nint;
-    g.nseg = 12 + nint;
-    for (int k = 0; k < nint; ++k) {
-        const double ax = iseg[k][0], ay = iseg[k][1], bx = iseg[k][2], by = iseg[k][3];
-        g.seg_ax[12 + k] = (float)ax;
-        g.seg_ay[12 + k] = (float)ay;
-        g.seg_sx[12 + k] = (float)bx - (float)ax;
-        g.seg_sy[12 + k] = (float)by - (float)ay;
-        const double abx = bx - ax, aby = by - ay, lsq = abx * abx + aby * aby, len = std::sqrt(lsq);
-        g.iw_nx[k] = (float)(-aby / len);
-        g.iw_ny[k] = (float)(abx / len);
-        g.iw_ax[k] = (float)ax;
-        g.iw_ay[k] = (float)ay;
-        g.iw_tx[k] = (float)abx;
-        g.iw_ty[k] = (float)aby;
-        g.iw_lsq[k] = (float)lsq;
-    }
-    const bool shelter = p.mission == SWARM_MISSION_SHELTERING;
-    g.iw_clear_tunnel = (float)(r + 0.5 * (shelter ? 0.03 : 0.0) + 1e-4);  // DG:909-913
-    g.iw_clear_capsule = (float)(r + 0.5 * (shelter ? 0.03 : 0.01) + 1e-4); // DG:981-990
-
-    g.gate_hw_neg = (float)(-corr_hw);
-    g.gate_hw_pos = (float)corr_hw;
-    g.gate_y0 = (float)gate_south;
-    g.gate_y1 = (float)(gate_south + 0.50);
-    const double t = 0.03;                                                  // SHC:27
-    g.sh_l = (float)sh_l;
-    g.sh_r = (float)sh_r;
-    g.sh_b = (float)sh_b;
-    g.sh_t = (float)sh_t;
-    g.sh_half = (float)(r + t / 2);
-    g.sh_bmr = (float)(sh_b - r);
-    g.sh_tpr = (float)(sh_t + r);
-    g.sh_lmr = (float)(sh_l - r);
-    g.sh_rpr = (float)(sh_r + r);
-
-    g.z_gate_hw = (float)gate_hw;
-    g.z_gate_south = (float)gate_south;
-    g.z_corr_south = (float)corr_south;
-    g.z_corr_hw = (float)corr_hw;
-    g.z_ni = (float)ni;
-    g.z_nest_top = (float)(mc ? -0.63 : -0.58);                             // MC:162 / FOC:28
-    g.goal_x = 0.0f;                                                        // HMC:24-25
-    g.goal_y = -0.70f;
-    switch (p.mission) {
-    case SWARM_MISSION_XOR: g.disc_x0 = -0.50f; g.disc_x1 = 0.50f; g.disc_r2 = (float)(0.30 * 0.30); break;
-    case SWARM_MISSION_FORAGING: g.disc_x0 = -0.75f; g.disc_x1 = 0.75f; break;
-    case SWARM_MISSION_SHELTERING: g.disc_x0 = -0.80f; g.disc_x1 = 0.80f; g.disc_r2 = (float)(0.30 * 0.30); break;
-    default: g.disc_r2 = (float)(0.30 * 0.30); break;
-    }
-    g.food_r = 0.15f;
-    g.food_r2 = (float)(0.15 * 0.15);
-
-    static const double div[8] = {10.5884, 3.5999, 2.0, 1.2, 0.8571, 0.6667, 0.5806, 0.5247};  // ES:28-37
-    for (int k = 0; k < 8; ++k) {
-        const float a = (float)(PI / div[k]);
-        g.cos_a[k] = std::cos(a);
-        g.sin_a[k] = -std::sin(a);                                          // ES:77
-    }
-    const float d2r = (float)(PI / 180.0);
-    for (int k = 0; k < 4; ++k) {
-        const float a = (45.0f + 90.0f * (float)k) * d2r;                   // ES:40-41
-        g.rab_cos[k] = std::cos(a);
-        g.rab_sin[k] = std::sin(a);
-    }
-    g.has_light = !(p.mission == SWARM_MISSION_HOMING || p.mission == SWARM_MISSION_XOR);
-    g.light_x = 0.0f;
-    g.light_y = mc ? -1.4f : -1.5f;                                         // MC:143 / DGC:171
-
-    // spawn (DGC:140-144; HMC:19-21; FOC/SHC:20-21) and MC:250-253
-    g.sp_cx = 0.0f; g.sp_cy = 0.0f; g.sp_sx = 2.4f; g.sp_sy = 2.4f; g.sp_rad = 1.2f;
-    if (p.mission == SWARM_MISSION_HOMING) { g.sp_cy = 0.7f; g.sp_sx = 2.0f; g.sp_sy = 0.6f; g.sp_rad = 0.8f; }
-    if (p.mission == SWARM_MISSION_FORAGING || p.mission == SWARM_MISSION_SHELTERING) {
-        g.sp_sx = 1.8f; g.sp_sy = 1.8f; g.sp_rad = 0.0f;
-    }
-    g.sp_attempts = 100;
-    g.mc_safe = (float)(ni - r * 2);
-    g.mc_th_scale = (float)(p.mission == SWARM_MISSION_HOMING ? PI : 2 * PI);
-
-    g.r_robot = (float)r;
-    g.min_dist = (float)(2 * r);
-    g.r2 = (float)(r * r);
-    g.max_speed = 0.16f;
-    g.wheelbase = 0.055f;
-    g.dt = 0.1f;
-    g.prox_range = 0.10f;
-    g.rab_range = 0.60f;
-    g.rab_loss = 0.85f;
-    g.unity = 0.10f;
-    g.light_thr = 0.2f;
-    g.light_int = 1000.0f;
-    g.alpha = 5.0f;
-    g.prox_thr = 0.1f;
-    g.pi_f = (float)PI;
-    g.two_pi_f = (float)(2.0 * PI);
-    g.half_pi_f = (float)(PI * 0.5);
-    g.critic_radius = 1.20f;
-    // fl(sqrt(s)) < x requires sqrt(s) < x, i.e. s < x^2; the margin keeps the
-    // float pre-filter a strict superset of the exact test (the kernels re-check).
-    g.min_dist2_hi = (float)((double)g.min_dist * g.min_dist * (1.0 + 1.0 / 1048576.0));
-    g.rab_range2_hi = (float)((double)g.rab_range * g.rab_range * (1.0 + 1.0 / 1048576.0));
-    g.inv_prox_range = 1.0f / g.prox_range;
-    g.inv_unity = 1.0f / g.unity;
-}
 
 DevState dev_state(const swarm_state_t* s) {
     return DevState{s->pos_x, s->pos_y, s->yaw, s->fsm, s->wheel_l, s->wheel_r, s->sensor_cache, s->ground_prev,
@@ -309,6 +133,17 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     if (!h) return SWARM_ERR_ARG;
     h->p = *p;
     build_geom(*p, h->g);
+    // the kernels use the compile-time tables generated from this same build_geom
+    // (gen_tables.cpp); refuse to run if the library was built from stale tables
+    {
+        const size_t off = offsetof(Geom, nseg);
+        const Geom& t = kGeomTab[p->mission][p->profile];
+        if (std::memcmp(reinterpret_cast<const char*>(&h->g) + off, reinterpret_cast<const char*>(&t) + off,
+                        sizeof(Geom) - off) != 0) {
+            delete h;
+            return SWARM_ERR_ABI;
+        }
+    }
     h->mirror.max_len = p->max_episode_length;
     h->lens.assign(p->num_envs, 0);
     h->mirror.assign(h->lens.data(), p->num_envs);

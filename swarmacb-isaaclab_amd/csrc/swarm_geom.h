@@ -21,58 +21,57 @@ enum RngPurpose : uint32_t {
     RNG_SPAWN_YAW = 9,     // yaw (DG:1260 / MC:258)
 };
 
+// Field list (X-macro): S(type, name) scalar, A(type, name, n) array. The same
+// list lays out the struct and drives tools' table generator (gen_tables.cpp),
+// which turns the host-built geometry of every (mission, profile) into
+// compile-time constants for the kernels (swarm_geom_tables.inc).
+#define SWARM_GEOM_FIELDS(S, A)                                                                             \
+    /* ---- layout (runtime: taken from the kernel argument) ---- */                                        \
+    S(int32_t, mission) S(int32_t, profile) S(int32_t, N) S(int32_t, E)                                     \
+    S(int32_t, obs_dim) S(int32_t, discrete) S(int32_t, max_len) S(int32_t, decimation)                     \
+    S(int32_t, apb)      /* arenas per 64-lane wave (= 64 / N) */                                            \
+    S(int32_t, layout)   /* work layout LY (swarm_step_impl.h): 1, 4 or 103 */                               \
+    S(uint32_t, seed_lo) S(uint32_t, seed_hi) S(uint32_t, env_off_lo) S(uint32_t, env_off_hi)               \
+    /* ---- mission constants (compile time in the kernels) ---- */                                          \
+    S(int32_t, nseg) S(int32_t, nint) /* raycast segments (arena 12 + internal), internal walls */           \
+    S(int32_t, has_light)                                                                                   \
+    /* raycast segments (torch.tensor(segments, float32), ES:205/474) */                                    \
+    A(float, seg_ax, 15) A(float, seg_ay, 15) A(float, seg_sx, 15) A(float, seg_sy, 15)                     \
+    /* arena faces DG:849-872 and MC:536-544 (its own mid angle) */                                          \
+    A(float, face_nx, 12) A(float, face_ny, 12) A(float, face_px, 12) A(float, face_py, 12)                 \
+    A(float, mcf_nx, 12) A(float, mcf_ny, 12) A(float, mcf_px, 12) A(float, mcf_py, 12)                     \
+    S(float, wall_clear_dg) /* r + 0.5*t + eps (DG:1050-1054) */                                             \
+    S(float, wall_clear_mc) /* r (MC:533) */                                                                 \
+    /* internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 */                                      \
+    A(float, iw_nx, 3) A(float, iw_ny, 3) A(float, iw_ax, 3) A(float, iw_ay, 3) A(float, iw_tx, 3)          \
+    A(float, iw_ty, 3) A(float, iw_lsq, 3) S(float, iw_clear_tunnel) S(float, iw_clear_capsule)             \
+    /* axis-aligned gate walls (DG:658-705), shelter walls (SH:124-155, MC:471-496) */                       \
+    S(float, gate_hw_neg) S(float, gate_hw_pos) S(float, gate_y0) S(float, gate_y1)                         \
+    S(float, sh_l) S(float, sh_r) S(float, sh_b) S(float, sh_t) S(float, sh_half) S(float, sh_bmr)          \
+    S(float, sh_tpr) S(float, sh_lmr) S(float, sh_rpr)                                                      \
+    /* ground zones; goal / targets / shelter discs (r^2), food / nest */                                   \
+    S(float, z_gate_hw) S(float, z_gate_south) S(float, z_corr_south) S(float, z_corr_hw) S(float, z_ni)    \
+    S(float, z_nest_top) S(float, goal_x) S(float, goal_y) S(float, disc_r2) S(float, disc_x0)              \
+    S(float, disc_x1) S(float, food_r) S(float, food_r2)                                                    \
+    /* sensors (ES:28-41, 75-79) */                                                                          \
+    A(float, cos_a, 8) A(float, sin_a, 8) A(float, rab_cos, 4) A(float, rab_sin, 4)                         \
+    S(float, light_x) S(float, light_y)                                                                     \
+    /* spawn (DGC:140-144 / mission cfgs; MC:250-258) */                                                     \
+    S(float, sp_cx) S(float, sp_cy) S(float, sp_sx) S(float, sp_sy) S(float, sp_rad) S(int32_t, sp_attempts) \
+    S(float, mc_safe) S(float, mc_th_scale)                                                                 \
+    /* scalar constants; squared pre-filters: s >= x2_hi guarantees fl(sqrt(s)) >= x */                     \
+    S(float, r_robot) S(float, min_dist) S(float, r2) S(float, max_speed) S(float, wheelbase) S(float, dt)  \
+    S(float, min_dist2_hi) S(float, rab_range2_hi) S(float, inv_prox_range) S(float, inv_unity)             \
+    S(float, prox_range) S(float, rab_range) S(float, rab_loss) S(float, unity) S(float, light_thr)         \
+    S(float, light_int) S(float, alpha) S(float, prox_thr) S(float, pi_f) S(float, two_pi_f)                \
+    S(float, half_pi_f) S(float, critic_radius)
+
 struct Geom {
-    // ---- layout ----
-    int32_t mission, profile, N, E;
-    int32_t obs_dim, discrete, max_len, decimation;
-    int32_t apb;            // arenas per 64-lane wave (= 64 / N)
-    int32_t layout;         // workgroup layout LY (swarm_step_impl.h): 1, 2, 4 waves or 103
-    int32_t nseg, nint;     // raycast segments (arena 12 + internal), internal walls
-    int32_t has_light;
-    uint32_t seed_lo, seed_hi;
-    uint32_t env_off_lo, env_off_hi;
-
-    // ---- raycast segments (torch.tensor(segments, float32), ES:205/474) ----
-    float seg_ax[15], seg_ay[15], seg_sx[15], seg_sy[15];
-
-    // ---- arena faces ----
-    float face_nx[12], face_ny[12], face_px[12], face_py[12];   // DG:849-872
-    float mcf_nx[12], mcf_ny[12], mcf_px[12], mcf_py[12];       // MC:536-544 (its own mid angle)
-    float wall_clear_dg;    // r + 0.5*t + eps (DG:1050-1054)
-    float wall_clear_mc;    // r (MC:533)
-
-    // ---- internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 ----
-    float iw_nx[3], iw_ny[3], iw_ax[3], iw_ay[3], iw_tx[3], iw_ty[3], iw_lsq[3];
-    float iw_clear_tunnel, iw_clear_capsule;
-
-    // ---- axis-aligned gate walls (DG:658-705) ----
-    float gate_hw_neg, gate_hw_pos, gate_y0, gate_y1;
-    // ---- shelter walls (SH:124-155, MC:471-496) ----
-    float sh_l, sh_r, sh_b, sh_t, sh_half, sh_bmr, sh_tpr, sh_lmr, sh_rpr;
-
-    // ---- ground zones ----
-    float z_gate_hw, z_gate_south, z_corr_south, z_corr_hw, z_ni, z_nest_top;
-    float goal_x, goal_y, disc_r2;              // homing goal / xor targets / shelter discs: r^2
-    float disc_x0, disc_x1;                     // xor targets / food / shelter black-disc centres (y = 0)
-    float food_r, food_r2;
-
-    // ---- sensors (ES:28-41, 75-79) ----
-    float cos_a[8], sin_a[8];
-    float rab_cos[4], rab_sin[4];
-    float light_x, light_y;
-
-    // ---- spawn (DGC:140-144 / mission cfgs; MC:250-258) ----
-    float sp_cx, sp_cy, sp_sx, sp_sy, sp_rad;
-    int32_t sp_attempts;
-    float mc_safe, mc_th_scale;
-
-    // ---- scalar constants ----
-    float r_robot, min_dist, r2, max_speed, wheelbase, dt;
-    // squared-distance pre-filters: s >= x2_hi guarantees fl(sqrt(s)) >= x (x^2 (1 + 2^-20))
-    float min_dist2_hi, rab_range2_hi;
-    float inv_prox_range, inv_unity;  // 1/0.1 rounded to float (= 10)
-    float prox_range, rab_range, rab_loss, unity, light_thr, light_int, alpha, prox_thr;
-    float pi_f, two_pi_f, half_pi_f, critic_radius;
+#define SWARM_GEOM_S(t, n) t n;
+#define SWARM_GEOM_A(t, n, k) t n[k];
+    SWARM_GEOM_FIELDS(SWARM_GEOM_S, SWARM_GEOM_A)
+#undef SWARM_GEOM_S
+#undef SWARM_GEOM_A
 };
 
 }  // namespace swarm

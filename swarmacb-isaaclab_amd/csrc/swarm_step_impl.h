@@ -55,6 +55,9 @@
 
 namespace swarm {
 
+// kGeomTab[mission][profile]: compile-time copy of build_geom() (gen_tables.cpp)
+#include "swarm_geom_tables.inc"
+
 // ---------------------------------------------------------------------------
 //  Philox4x32-10 (counter-based: results depend only on (seed, counter), so
 //  they are identical however the envs are sharded over GPUs or blocks).
@@ -71,11 +74,9 @@ __device__ __forceinline__ uint4 philox4x32(uint4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-__device__ __forceinline__ uint4 rng4(const Geom& g, uint32_t genv, uint32_t robot, uint32_t block,
-                                      uint32_t purpose, uint64_t tick) {
-    uint4 c = make_uint4(genv, robot | (block << 8) | (purpose << 24), (uint32_t)tick, (uint32_t)(tick >> 32));
-    return philox4x32(c, g.seed_lo, g.seed_hi);
-}
+struct Lane;
+__device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t block, uint32_t purpose,
+                                      uint64_t tick);
 
 // torch-style float uniform from 24 random bits: [0, 1)
 __device__ __forceinline__ float u01(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
@@ -171,7 +172,16 @@ struct Lane {
     bool valid;
     uint32_t genv;
     unsigned long long amask;  // ballot bits of this arena's part-0 lanes
+    int E, obs_dim;            // runtime layout (kernel argument)
+    uint32_t seed_lo, seed_hi;
 };
+
+// Philox counter (global env, robot | block << 8 | purpose << 24, tick), key = seed.
+__device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t block, uint32_t purpose,
+                                      uint64_t tick) {
+    uint4 c = make_uint4(L.genv, robot | (block << 8) | (purpose << 24), (uint32_t)tick, (uint32_t)(tick >> 32));
+    return philox4x32(c, L.seed_lo, L.seed_hi);
+}
 
 // LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
 // broadcast within an arena) and 4 float4 partial slots per thread.
@@ -691,7 +701,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
                 uu = cnd[jj] ? u_replay[min(j, L.N - 1)] : 0.0f;
             } else {
                 if (ChunkRng<C>::fresh(jj))
-                    rb = rng4(g, L.genv, (uint32_t)L.i, ChunkRng<C>::block(L.p, jj), purpose, tick);
+                    rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, jj), purpose, tick);
                 uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
             }
             if (cnd[jj] && uu >= g.rab_loss) term(j, p[jj].x - x, p[jj].y - y);
@@ -720,7 +730,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
                 const uint32_t b = ChunkRng<C>::block(L.p, jj);
                 if (b != blk) {
                     blk = b;
-                    rb = rng4(g, L.genv, (uint32_t)L.i, blk, purpose, tick);
+                    rb = rng4(L, (uint32_t)L.i, blk, purpose, tick);
                 }
                 uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
             }
@@ -762,7 +772,7 @@ struct TurnSrc {
 
 __device__ __forceinline__ int draw_turn(const Geom& g, const Lane& L, const TurnSrc& ts, int slot) {
     if (ts.replay) return ts.replay[(size_t)slot * ts.slot_stride + ts.q];
-    const uint4 r = rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_TURN + (uint32_t)slot, ts.tick);
+    const uint4 r = rng4(L, (uint32_t)L.i, 0u, RNG_TURN + (uint32_t)slot, ts.tick);
     return 1 + (int)(r.x & 3u);
 }
 
@@ -964,8 +974,8 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     agg.ay = ayy;
     if (L.valid && obs) {
         const float gv = 0.5f * (float)ground_code<MISSION, PROFILE>(g, x, y);
-        float* o = obs + ((uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i) * (uint32_t)g.obs_dim;
-        if (g.obs_dim == 24) {
+        float* o = obs + ((uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i) * (uint32_t)L.obs_dim;
+        if (L.obs_dim == 24) {
             float4* o4 = reinterpret_cast<float4*>(o);
             // chunk c of the 24-D row is stored by part c % P
 #pragma unroll
@@ -1017,11 +1027,11 @@ __device__ __forceinline__ void spawn_isaac(const Geom& g, const Lane& L, const 
         }
         float u0, u1;
         if (rp.spawn) {
-            const float* p = rp.spawn + (((size_t)k * g.E) * L.N + q) * 2;
+            const float* p = rp.spawn + (((size_t)k * L.E) * L.N + q) * 2;
             u0 = p[0];
             u1 = p[1];
         } else {
-            if ((k & 1) == 0) rb = rng4(g, L.genv, (uint32_t)L.i, (uint32_t)(k >> 1), RNG_SPAWN, tick);
+            if ((k & 1) == 0) rb = rng4(L, (uint32_t)L.i, (uint32_t)(k >> 1), RNG_SPAWN, tick);
             u0 = u01((k & 1) ? rb.z : rb.x);
             u1 = u01((k & 1) ? rb.w : rb.y);
         }
@@ -1030,7 +1040,7 @@ __device__ __forceinline__ void spawn_isaac(const Geom& g, const Lane& L, const 
         if (!rej) break;
     }
     const float uy = rp.spawn_yaw ? rp.spawn_yaw[q]
-                                  : u01(rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_SPAWN_YAW, tick).x);
+                                  : u01(rng4(L, (uint32_t)L.i, 0u, RNG_SPAWN_YAW, tick).x);
     yaw = uy * 2.0f * g.pi_f - g.pi_f;
 }
 
@@ -1041,12 +1051,12 @@ __device__ __forceinline__ void spawn_mc(const Geom& g, const Lane& L, const Dev
     float ur, ut, uy;
     const size_t q = (size_t)L.env * L.N + L.i;
     if (rp.spawn) {
-        const size_t EN = (size_t)g.E * L.N;
+        const size_t EN = (size_t)L.E * L.N;
         ur = rp.spawn[q];
         ut = rp.spawn[EN + q];
         uy = rp.spawn[2 * EN + q];
     } else {
-        const uint4 r = rng4(g, L.genv, (uint32_t)L.i, 0u, RNG_SPAWN, tick);
+        const uint4 r = rng4(L, (uint32_t)L.i, 0u, RNG_SPAWN, tick);
         ur = u01(r.x);
         ut = u01(r.y);
         uy = u01(r.z);
@@ -1108,10 +1118,14 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 // NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
 // every neighbour loop has a compile-time trip count and is fully unrolled.
 template <int NA, int LY>
-__device__ __forceinline__ Lane make_lane(const Geom& g) {
+__device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime kernel argument
     constexpr int KL = ly_lanes(LY), P = ly_parts(LY);
     Lane L;
     L.N = NA > 0 ? NA : g.N;
+    L.E = g.E;
+    L.obs_dim = g.obs_dim;
+    L.seed_lo = g.seed_lo;
+    L.seed_hi = g.seed_hi;
     const int lane = threadIdx.x & 63;
     L.tid = threadIdx.x;
     int apb;                                      // arenas per wave
@@ -1155,15 +1169,16 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {
 // null, so the replay-only paths (parity tests) cost it no registers or code.
 template <int MISSION, int PROFILE, bool DISCRETE, int NA, int LY, bool REPLAY>
 __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void step_kernel(
-    const Geom g, const DevState st, const void* __restrict__ actions, const float* __restrict__ ovr,
+    const Geom gr, const DevState st, const void* __restrict__ actions, const float* __restrict__ ovr,
     const DevOut out, const DevReplay rp_in, uint64_t tick0, int n_sub, uint64_t reset_any) {
     const DevReplay rp = REPLAY ? rp_in : DevReplay{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+    const Geom& g = kGeomTab[MISSION][PROFILE];   // mission constants as literals; gr: runtime fields
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
-    const Lane L = make_lane<NA, LY>(g);
+    const Lane L = make_lane<NA, LY>(gr);
     // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
     const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
-    const uint32_t EN = (uint32_t)g.E * (uint32_t)L.N;
+    const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
 
     // ---- load state (invalid lanes keep harmless values) ----
     float x = 0.0f, y = 0.0f, yaw = 0.0f, wl = 0.0f, wr = 0.0f;
@@ -1214,13 +1229,13 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     for (int s = 0; s < n_sub; ++s) {
         const uint64_t tick = tick0 + (uint64_t)s;
         const size_t NN = (size_t)L.N * L.N;
-        const float* u_obs = rp.rab ? rp.rab + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
+        const float* u_obs = rp.rab ? rp.rab + ((size_t)s * L.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
         TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, (size_t)EN, (size_t)q, tick};
 
         // ------------------------------ actions ------------------------------
         float lw, rw;
         if constexpr (PROFILE == STANDALONE) {
-            const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * g.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
+            const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * L.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
                                         : nullptr;
             rab_only<LY, C>(g, L, S, x, y, syaw, cyaw, u_d, tick, cache.ax, cache.ay);
             if constexpr (DISCRETE) {
@@ -1251,14 +1266,14 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         if constexpr (PROFILE == ISAAC) {
             // decimation x {integrate, contacts}, then dones / rewards / auto-reset,
             // then (if any env of the batch reset) the solver again on all envs.
-            for (int d = 0; d < g.decimation; ++d) {
+            for (int d = 0; d < gr.decimation; ++d) {
                 const float qx = x, qy = y;
                 if (d > 0) sincosf(yaw, &syaw, &cyaw);
                 integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
                 if (!(SWARM_ABLATE & 16)) solve<MISSION, LY, C, true>(g, L, S, x, y, qx, qy);
             }
             ep_len += 1;
-            tout = ep_len >= g.max_len;                                      // DG:1200-1209
+            tout = ep_len >= gr.max_len;                                     // DG:1200-1209
             if (tout && L.valid && L.p == 0) {
                 float c5[5];
                 critic5(g, x, y, yaw, c5);
@@ -1287,11 +1302,11 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             walls_mc(g, x, y);
             gate_walls<MISSION, STANDALONE>(g, x, y);
             robots_push<LY, C>(g, L, S, x, y);
-            const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, ep_len + 1 >= g.max_len);
+            const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, ep_len + 1 >= gr.max_len);
             ep_rew += r;
             rew_acc += r;
             ep_len += 1;
-            tout = ep_len >= g.max_len;                                      // MC:753-754
+            tout = ep_len >= gr.max_len;                                     // MC:753-754
             if (tout) {
                 comp = ep_rew;
                 if (L.valid) spawn_mc<MISSION>(g, L, rp, tick, x, y, yaw);
@@ -1338,14 +1353,15 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 //  Reset kernel: _reset_idx(mask) + observations (DirectMARLEnv.reset)
 // ---------------------------------------------------------------------------
 template <int MISSION, int PROFILE, int NA>
-__global__ __launch_bounds__(64) void reset_kernel(const Geom g, const DevState st, const uint8_t* __restrict__ mask,
+__global__ __launch_bounds__(64) void reset_kernel(const Geom gr, const DevState st, const uint8_t* __restrict__ mask,
                                                    const DevOut out, const DevReplay rp, uint64_t tick) {
     constexpr int LY = 1;
     constexpr int C = NA > 0 ? NA : 0;
+    const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY> S;
-    const Lane L = make_lane<NA, LY>(g);
+    const Lane L = make_lane<NA, LY>(gr);
     const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
-    const size_t EN = (size_t)g.E * L.N;
+    const size_t EN = (size_t)L.E * L.N;
     float x = 0.0f, y = 0.0f, yaw = 0.0f;
     bool doit = false;
     if (L.valid) {
