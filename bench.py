@@ -53,7 +53,11 @@ def parse():
     ap.add_argument("--layout", type=int, default=0,
                     help="kernel work layout (1/2/4 waves per 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
-    return ap.parse_args()
+    ap.add_argument("--rollout", action="store_true",
+                    help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
+    args, rest = ap.parse_known_args()
+    args.rest = rest
+    return args
 
 
 def cpu_baseline(budget_s: float, envs: int) -> dict | None:
@@ -102,6 +106,13 @@ def load_pmc(envs: int, sub: int) -> dict:
 
 def main():
     args = parse()
+    if args.rollout:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_rollout
+
+        sys.argv = [sys.argv[0]] + args.rest
+        bench_rollout.main()
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

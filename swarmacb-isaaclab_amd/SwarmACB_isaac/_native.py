@@ -54,6 +54,17 @@ EXPORTS = [
     "swarm_fsm_pack",
 ]
 
+# Every symbol include/swarmrollout.h declares (rollout-buffer kernels, same library).
+ROLLOUT_EXPORTS = ["swarm_lambda_returns", "swarm_sequence_chunk_offsets", "swarm_sequence_chunk_fill", "swarm_gather"]
+
+GATHER_MAX_FIELDS = 48
+GATHER_KINDS = {"focal": 0, "group": 1, "focal_first": 2, "group_first": 3}
+
+
+class GatherField(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_words", C.c_int32), ("kind", C.c_int32)]
+
+
 _lib = None
 
 
@@ -89,6 +100,16 @@ def load() -> C.CDLL:
     lib.swarm_tick.argtypes = [C.c_void_p]
     lib.swarm_fsm_pack.restype = C.c_uint32
     lib.swarm_fsm_pack.argtypes = [C.c_int32, C.c_int32, C.c_float] * 3
+    i32, i64, vp = C.c_int32, C.c_int64, C.c_void_p
+    lib.swarm_lambda_returns.restype = i32
+    lib.swarm_lambda_returns.argtypes = [i32, i32, i32, C.c_double, C.c_double, vp, vp, vp, vp, vp, vp, i32,
+                                         C.POINTER(vp), vp, C.POINTER(vp), vp]
+    lib.swarm_sequence_chunk_offsets.restype = i32
+    lib.swarm_sequence_chunk_offsets.argtypes = [i32, i32, i32, i32, vp, vp, vp]
+    lib.swarm_sequence_chunk_fill.restype = i32
+    lib.swarm_sequence_chunk_fill.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp]
+    lib.swarm_gather.restype = i32
+    lib.swarm_gather.argtypes = [i32, C.POINTER(GatherField), i32, vp, vp, i32, i32, i32, i32, i32, i64, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

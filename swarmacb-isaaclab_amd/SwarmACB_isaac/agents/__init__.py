@@ -1,0 +1,10 @@
+"""Trainer-side callers of the e-puck step: the rollout
+buffers of the reference's three trainers (agents/poca_buffer.py,
+option_critic_buffer.py, learned_option_critic_buffer.py), same API, with the
+end-of-rollout scan and the minibatch gathers as HIP kernels."""
+
+from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
+from .option_critic_buffer import FixedOptionRolloutBuffer
+from .poca_buffer import POCARolloutBuffer
+
+__all__ = ["POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer"]

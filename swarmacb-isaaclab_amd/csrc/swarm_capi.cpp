@@ -101,6 +101,8 @@ int32_t hip_status() {
 
 }  // namespace
 
+int32_t swarm::record_hip_status() { return hip_status(); }
+
 extern "C" {
 
 int32_t swarm_abi_version(void) { return SWARM_ABI_VERSION; }

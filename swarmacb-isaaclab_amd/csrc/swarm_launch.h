@@ -43,6 +43,9 @@ void launch_step(const Geom& g, const DevState& st, const void* actions, const f
                  const DevReplay& rp, uint64_t tick, int n_sub, uint64_t reset_any, hipStream_t stream);
 void launch_reset(const Geom& g, const DevState& st, const uint8_t* mask, const DevOut& out, const DevReplay& rp,
                   uint64_t tick, hipStream_t stream);
+// hipGetLastError() -> SWARM_OK / SWARM_ERR_HIP (kept for swarm_last_hip_error)
+int32_t record_hip_status();
+
 void launch_critic(const Geom& g, const float* x, const float* y, const float* yaw, float* out, hipStream_t stream);
 
 }  // namespace swarm

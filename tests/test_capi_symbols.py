@@ -12,23 +12,25 @@ from conftest import ROOT
 from SwarmACB_isaac import _native
 from SwarmACB_isaac.engine import fsm_pack, fsm_unpack
 
-HEADER = os.path.join(ROOT, "include", "swarmstep.h")
+HEADERS = {"swarmstep.h": _native.EXPORTS, "swarmrollout.h": _native.ROLLOUT_EXPORTS}
 
 
-def declared_functions() -> list[str]:
-    text = open(HEADER).read()
+def declared_functions(header: str = "swarmstep.h") -> list[str]:
+    text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(swarm_[a-z_]+)\s*\(", text)))
 
 
-def test_header_and_binding_agree():
-    assert declared_functions() == sorted(_native.EXPORTS)
+@pytest.mark.parametrize("header", sorted(HEADERS))
+def test_header_and_binding_agree(header):
+    assert declared_functions(header) == sorted(HEADERS[header])
 
 
 def test_library_exports_every_declared_symbol():
     lib = _native.load()
-    for name in declared_functions():
-        assert hasattr(lib, name), name
+    for header in HEADERS:
+        for name in declared_functions(header):
+            assert hasattr(lib, name), name
     assert lib.swarm_abi_version() == _native.ABI_VERSION
     assert lib.swarm_strerror(0) == b"ok"
     assert lib.swarm_strerror(-1) == b"invalid argument"
