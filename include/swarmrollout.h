@@ -91,6 +91,53 @@ int32_t swarm_gather(int32_t mode, const swarm_gather_field_t* fields, int32_t n
                      int32_t E, int32_t N, int64_t n_items, float* loss_mask, int64_t* focal_ids,
                      void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Decision record (the per-decision glue of collect_rollout, poca_trainer.py:
+ * 575-634; same pattern option_critic_trainer.py:363-437,
+ * learned_option_critic_trainer.py:870-948): one call after the env's decision
+ * period replaces the reward scaling, done / time-out flags, timeout-value
+ * masking, episode accumulators, completed-episode bookkeeping (a host sync
+ * per decision in the reference: `done_mask.any()` + `.tolist()`) and the
+ * recurrent-memory resets of done envs.
+ *
+ *   rewards[e]        = reward_sum[e] * f32(reward_strength)
+ *   dones[e]          = timeouts[e] = truncated[e] ? 1 : 0   (terminated is always False)
+ *   timeout_values[e] = timeout_value_raw[e] * timeouts[e]
+ *   episode_reward[e] += reward_sum[e];  episode_steps[e] += decision_period
+ *   for done e, in increasing e: append (episode_reward, episode_steps,
+ *     completed_group_reward) to the log at log_count++ (dropped past
+ *     log_capacity; log_count still counts), then zero both accumulators
+ *   for done e: zero rows [e*rows_per_env, (e+1)*rows_per_env) of every memory slab
+ */
+#define SWARM_RECORD_MAX_MEMORIES 8
+
+typedef struct {
+    float* data;                  /* [E * rows_per_env * width] */
+    int32_t rows_per_env;         /* N for per-agent memories, 1 for per-env (critic) memories */
+    int32_t width;
+} swarm_memory_slab_t;
+
+typedef struct {
+    float* rewards;               /* buffer row t [E] */
+    float* dones;                 /* [E] */
+    float* timeouts;              /* [E] */
+    float* timeout_values;        /* [E], nullable (then timeout_value_raw is ignored) */
+    float* episode_reward;        /* trainer accumulators [E] */
+    float* episode_steps;         /* [E] */
+    float* log_returns;           /* [log_capacity], nullable */
+    float* log_lengths;           /* [log_capacity], nullable */
+    float* log_group_rewards;     /* [log_capacity], nullable */
+    int32_t* log_count;           /* device int32[1] */
+    int32_t log_capacity;
+    int32_t n_memories;
+    swarm_memory_slab_t memories[SWARM_RECORD_MAX_MEMORIES];
+} swarm_decision_record_t;
+
+int32_t swarm_decision_record(int32_t E, int32_t decision_period, double reward_strength,
+                              const float* reward_sum, const uint8_t* truncated,
+                              const float* timeout_value_raw, const float* completed_group_reward,
+                              const swarm_decision_record_t* rec, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -55,7 +55,8 @@ EXPORTS = [
 ]
 
 # Every symbol include/swarmrollout.h declares (rollout-buffer kernels, same library).
-ROLLOUT_EXPORTS = ["swarm_lambda_returns", "swarm_sequence_chunk_offsets", "swarm_sequence_chunk_fill", "swarm_gather"]
+ROLLOUT_EXPORTS = ["swarm_lambda_returns", "swarm_sequence_chunk_offsets", "swarm_sequence_chunk_fill", "swarm_gather",
+                   "swarm_decision_record"]
 
 GATHER_MAX_FIELDS = 48
 GATHER_KINDS = {"focal": 0, "group": 1, "focal_first": 2, "group_first": 3}
@@ -63,6 +64,20 @@ GATHER_KINDS = {"focal": 0, "group": 1, "focal_first": 2, "group_first": 3}
 
 class GatherField(C.Structure):
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_words", C.c_int32), ("kind", C.c_int32)]
+
+
+RECORD_MAX_MEMORIES = 8
+
+
+class MemorySlab(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("rows_per_env", C.c_int32), ("width", C.c_int32)]
+
+
+class DecisionRecord(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "timeouts", "timeout_values", "episode_reward",
+                                          "episode_steps", "log_returns", "log_lengths", "log_group_rewards",
+                                          "log_count")] + [
+        ("log_capacity", C.c_int32), ("n_memories", C.c_int32), ("memories", MemorySlab * RECORD_MAX_MEMORIES)]
 
 
 _lib = None
@@ -110,6 +125,8 @@ def load() -> C.CDLL:
     lib.swarm_sequence_chunk_fill.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp]
     lib.swarm_gather.restype = i32
     lib.swarm_gather.argtypes = [i32, C.POINTER(GatherField), i32, vp, vp, i32, i32, i32, i32, i32, i64, vp, vp, vp]
+    lib.swarm_decision_record.restype = i32
+    lib.swarm_decision_record.argtypes = [i32, i32, C.c_double, vp, vp, vp, vp, C.POINTER(DecisionRecord), vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -3,8 +3,9 @@ buffers of the reference's three trainers (agents/poca_buffer.py,
 option_critic_buffer.py, learned_option_critic_buffer.py), same API, with the
 end-of-rollout scan and the minibatch gathers as HIP kernels."""
 
+from .collector import DecisionRecorder, POCARolloutCollector
 from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
 from .option_critic_buffer import FixedOptionRolloutBuffer
 from .poca_buffer import POCARolloutBuffer
 
-__all__ = ["POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer"]
+__all__ = ["DecisionRecorder", "POCARolloutCollector", "POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer"]

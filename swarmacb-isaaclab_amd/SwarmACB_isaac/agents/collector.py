@@ -1,0 +1,215 @@
+"""Decision loop glue: the caller of the e-puck step on the trainer side
+(poca_trainer.py:441-649 ``collect_rollout``).
+
+Per ML-Agents decision the reference stacks 20 obs views, samples the shared
+actor, evaluates the critic and the counterfactual baselines, steps the env
+``decision_period`` times through 20-entry action dicts, accumulates reward /
+done / time-out with ~10 small tensor ops, snapshots the terminal critic
+state, appends one buffer row, and does the episode bookkeeping with a host
+sync (``done_mask.any()`` + ``.tolist()``). Here:
+
+* the env's decision period is ONE launch of the step kernel
+  (``env.step_decision``) that writes its observation straight into the
+  rollout buffer's next row (no dict split / stack);
+* the critic state is written by its kernel straight into the buffer row;
+* the post-step bookkeeping is ONE launch (``swarm_decision_record``): reward
+  scaling, done / time-out flags, time-out values, episode accumulators, the
+  completed-episode log (kept on the device, in the reference's env order,
+  drained without a per-decision sync) and the LSTM-memory resets;
+* the policy and critic evaluations stay PyTorch (duck-typed like the
+  reference: ``actor.get_dist`` / ``actor.step``, ``critic.critic_pass`` /
+  ``critic.all_baselines``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .. import _native
+from ._rollout import _dev_check, _p, _stream
+
+
+class DecisionRecorder:
+    """Device-side episode bookkeeping of a trainer (poca_trainer.py:363-367, 605-634)."""
+
+    def __init__(self, num_envs: int, device, log_capacity: int | None = None):
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device)
+        cap = int(log_capacity if log_capacity is not None else max(1024, 64 * self.num_envs))
+        z = lambda n: torch.zeros(n, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.episode_reward = z(self.num_envs)   # _episode_reward_acc
+        self.episode_steps = z(self.num_envs)    # _episode_step_count
+        self.log_returns, self.log_lengths, self.log_group = z(cap), z(cap), z(cap)
+        self.log_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.capacity = cap
+
+    def record(self, row: dict, reward_sum, truncated, completed_group_reward, decision_period: int,
+               reward_strength: float, timeout_value_raw=None, memories=()):
+        """row: {"rewards", "dones", "timeouts"[, "timeout_values"]} -> (E,) float32 views of
+        the buffer row being written. memories: [(tensor, rows_per_env)], rows of done envs
+        are zeroed."""
+        E = self.num_envs
+        rec = _native.DecisionRecord()
+        rec.rewards, rec.dones, rec.timeouts = (row["rewards"].data_ptr(), row["dones"].data_ptr(),
+                                                row["timeouts"].data_ptr())
+        tv = row.get("timeout_values")
+        rec.timeout_values = tv.data_ptr() if tv is not None else None
+        rec.episode_reward, rec.episode_steps = self.episode_reward.data_ptr(), self.episode_steps.data_ptr()
+        rec.log_returns, rec.log_lengths = self.log_returns.data_ptr(), self.log_lengths.data_ptr()
+        rec.log_group_rewards, rec.log_count = self.log_group.data_ptr(), self.log_count.data_ptr()
+        rec.log_capacity = self.capacity
+        if len(memories) > _native.RECORD_MAX_MEMORIES:
+            raise ValueError("too many memory slabs")
+        rec.n_memories = len(memories)
+        for i, (m, rows) in enumerate(memories):
+            _dev_check(m)
+            width = m.numel() // (E * rows)
+            if width * E * rows != m.numel():
+                raise ValueError("memory slab is not (E*rows, width)")
+            rec.memories[i] = _native.MemorySlab(m.data_ptr(), rows, width)
+        tensors = [reward_sum, truncated, completed_group_reward, timeout_value_raw] + list(row.values())
+        _dev_check(*tensors)
+        if truncated.dtype not in (torch.uint8, torch.bool):
+            raise ValueError("truncated must be uint8/bool")
+        rc = _native.load().swarm_decision_record(
+            E, int(decision_period), float(reward_strength), _p(reward_sum), _p(truncated),
+            _p(timeout_value_raw), _p(completed_group_reward), C.byref(rec), _stream(reward_sum))
+        _native.check(rc, "swarm_decision_record")
+
+    def drain(self):
+        """Completed (returns, lengths, group rewards) since the last drain, in the
+        reference's order (one device->host copy)."""
+        n = int(self.log_count.item())
+        if n > self.capacity:
+            raise RuntimeError(f"completed-episode log overflowed ({n} > {self.capacity}); raise log_capacity")
+        out = (self.log_returns[:n].tolist(), self.log_lengths[:n].tolist(), self.log_group[:n].tolist())
+        self.log_count.zero_()
+        return out
+
+
+class POCARolloutCollector:
+    """``collect_rollout`` of poca_trainer.py:441-649 over the MI355X env and buffer.
+
+    env: a SwarmACB_isaac env (``step_decision``, ``get_critic_state``, ...);
+    buffer: agents.POCARolloutBuffer; actor / critic: duck-typed like the
+    reference's (poca_networks.py). ``obs`` is the (E, N, D) observation the
+    first decision is taken on (env.reset()'s, stacked)."""
+
+    def __init__(self, env, buffer, actor, critic, *, decision_period: int, reward_strength: float = 1.0,
+                 discrete: bool = False, num_actions: int = 0, recurrent: bool = False):
+        self.env, self.buffer, self.actor, self.critic = env, buffer, actor, critic
+        self.decision_period = int(decision_period)
+        self.reward_strength = float(reward_strength)
+        self.discrete, self.num_actions, self.recurrent = discrete, num_actions, recurrent
+        self.num_envs, self.num_agents = env.num_envs, env.num_agents
+        self.device = env.device
+        self.recorder = DecisionRecorder(self.num_envs, self.device)
+        self.global_step = 0
+        E, N = self.num_envs, self.num_agents
+        self._obs = torch.zeros(E, N, buffer.obs_dim, device=self.device)
+        self._rew = torch.zeros(E, device=self.device)
+        self._trunc = torch.zeros(E, dtype=torch.uint8, device=self.device)
+        if recurrent:
+            ah, ch = actor.hidden_size, critic.hidden_size
+            z = lambda *s: torch.zeros(*s, device=self.device)  # noqa: E731
+            self.actor_memory_h, self.actor_memory_c = z(1, E * N, ah), z(1, E * N, ah)
+            self.critic_memory_h, self.critic_memory_c = z(1, E, ch), z(1, E, ch)
+            self.baseline_memory_h, self.baseline_memory_c = z(1, E * N, ch), z(1, E * N, ch)
+
+    def _encode_actions_for_critic(self, actions):
+        """poca_trainer.py:406-419."""
+        if self.discrete:
+            return torch.nn.functional.one_hot(actions.squeeze(-1).long(), self.num_actions).float()
+        return actions
+
+    @torch.no_grad()
+    def collect(self, obs: torch.Tensor, rollout_steps: int, reset_buffer: bool = True) -> torch.Tensor:
+        buf, E, N, dp = self.buffer, self.num_envs, self.num_agents, self.decision_period
+        if reset_buffer:
+            buf.reset()
+        for _ in range(int(rollout_steps)):
+            t = buf.ptr
+            if t >= buf.horizon:
+                raise RuntimeError(buf._full_message)
+            flat_obs = obs.reshape(E * N, -1)
+            memory_h = memory_c = None
+            if self.recurrent:
+                memory_h = self.actor_memory_h.squeeze(0).view(E, N, -1).clone()
+                memory_c = self.actor_memory_c.squeeze(0).view(E, N, -1).clone()
+                logits, nm = self.actor.step(flat_obs, (self.actor_memory_h, self.actor_memory_c))
+                self.actor_memory_h, self.actor_memory_c = nm[0].detach(), nm[1].detach()
+                dist = torch.distributions.Categorical(logits=logits)
+            else:
+                dist = self.actor.get_dist(flat_obs)
+            flat_act = dist.sample()
+            flat_logp = dist.log_prob(flat_act)
+            act_dim = 1 if self.discrete else buf.act_dim
+            all_actions = flat_act.view(E, N, act_dim)
+            all_log_probs = flat_logp.view(E, N, act_dim)
+
+            # the critic-state kernel writes straight into buffer row t (DG:1279-1290)
+            critic_state = self.env.engine.critic_state(out=buf.critic_states[t]) \
+                if hasattr(self.env, "engine") else self.env.get_critic_state()
+            critic_actions = self._encode_actions_for_critic(all_actions)
+            cmh = cmc = bmh = bmc = None
+            if self.recurrent:
+                cmh, cmc = self.critic_memory_h.squeeze(0).clone(), self.critic_memory_c.squeeze(0).clone()
+                bmh = self.baseline_memory_h.squeeze(0).view(E, N, -1).clone()
+                bmc = self.baseline_memory_c.squeeze(0).view(E, N, -1).clone()
+                team_val, ncm = self.critic.critic_pass(critic_state, (self.critic_memory_h, self.critic_memory_c),
+                                                        return_memory=True)
+                baselines, nbm = self.critic.all_baselines(
+                    critic_state, critic_actions, (self.baseline_memory_h, self.baseline_memory_c),
+                    return_memory=True)
+                self.critic_memory_h, self.critic_memory_c = ncm[0].detach(), ncm[1].detach()
+                self.baseline_memory_h, self.baseline_memory_c = nbm[0].detach(), nbm[1].detach()
+                team_val = team_val.squeeze(-1)
+            else:
+                team_val = self.critic.critic_pass(critic_state).squeeze(-1)
+                baselines = self.critic.all_baselines(critic_state, critic_actions)
+
+            env_actions = all_actions if self.discrete else all_actions.clamp(-3, 3) / 3
+            # store the pre-decision row, then one launch for the whole decision period
+            if obs.data_ptr() != buf.obs[t].data_ptr():
+                buf.obs[t] = obs
+            if critic_state.data_ptr() != buf.critic_states[t].data_ptr():
+                buf.critic_states[t] = critic_state
+            buf.actions[t] = all_actions
+            buf.log_probs[t] = all_log_probs
+            buf.team_values[t] = team_val
+            buf.baselines[t] = baselines
+            if self.recurrent:
+                buf.memory_h[t], buf.memory_c[t] = memory_h, memory_c
+                if buf.critic_memory_size > 0:
+                    buf.critic_memory_h[t], buf.critic_memory_c[t] = cmh, cmc
+                    buf.baseline_memory_h[t], buf.baseline_memory_c[t] = bmh, bmc
+            # the step writes the next decision's observation straight into buffer row t+1
+            obs_out = buf.obs[t + 1] if t + 1 < buf.horizon else self._obs
+            obs_next, rew, trunc = self.env.step_decision(env_actions, dp, out=(obs_out, self._rew, self._trunc))
+
+            terminal = self.env.completed_terminal_critic_state
+            if self.recurrent:
+                tv = self.critic.critic_pass(terminal, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
+            else:
+                tv = self.critic.critic_pass(terminal).squeeze(-1)
+            mems = []
+            if self.recurrent:
+                mems = [(self.actor_memory_h, N), (self.actor_memory_c, N), (self.critic_memory_h, 1),
+                        (self.critic_memory_c, 1), (self.baseline_memory_h, N), (self.baseline_memory_c, N)]
+            self.recorder.record(
+                {"rewards": buf.rewards[t], "dones": buf.dones[t], "timeouts": buf.timeouts[t],
+                 "timeout_values": buf.timeout_values[t]},
+                rew, trunc, self.env.completed_group_reward, dp, self.reward_strength,
+                timeout_value_raw=tv.contiguous(), memories=mems)
+            buf.ptr = t + 1
+            obs = obs_next
+            self.global_step += E * N
+        last_state = self.env.get_critic_state()
+        if self.recurrent:
+            last_tv = self.critic.critic_pass(last_state, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
+        else:
+            last_tv = self.critic.critic_pass(last_state).squeeze(-1)
+        buf.compute_returns_and_advantages(last_tv)
+        return obs.clone()

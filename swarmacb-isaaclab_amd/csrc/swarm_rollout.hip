@@ -127,7 +127,7 @@ __device__ inline void for_each_window(int T, int E, int L, int e, const float* 
     for (int s = seg; s < T; s += L) f(s, min(s + L, T));
 }
 
-__global__ void __launch_bounds__(256) chunk_count_kernel(int T, int E, int N, int L,
+__global__ void __launch_bounds__(64) chunk_count_kernel(int T, int E, int N, int L,
                                                           const float* __restrict__ dones, int32_t* counts) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= E) return;
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(1024) exclusive_scan_kernel(int E, int32_t* co
     if (tid == 1023) counts[E] = part[1023];
 }
 
-__global__ void __launch_bounds__(256) chunk_fill_kernel(int T, int E, int N, int L, const float* __restrict__ dones,
+__global__ void __launch_bounds__(64) chunk_fill_kernel(int T, int E, int N, int L, const float* __restrict__ dones,
                                                          const int32_t* __restrict__ offsets,
                                                          int4* __restrict__ chunks) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -275,9 +275,105 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherFields fl, int n_fiel
         gather_field<uint32_t>(F, 1, mode, base, blockDim.x, chunks, order, B, L, E, N, n_items);
 }
 
+// ---------------------------------------------------------------------------
+//  Decision record (poca_trainer.py:575-634). One workgroup walks the envs in
+//  order (each thread a contiguous range, then a block scan of the done
+//  counts) so the completed-episode log keeps the reference's env order.
+// ---------------------------------------------------------------------------
+struct RecordArgs {
+    swarm_decision_record_t r;
+};
+
+__global__ void __launch_bounds__(1024) record_kernel(RecordArgs a, int E, float dp, float strength,
+                                                      const float* __restrict__ rsum,
+                                                      const uint8_t* __restrict__ trunc,
+                                                      const float* __restrict__ tv_raw,
+                                                      const float* __restrict__ group) {
+    const swarm_decision_record_t& r = a.r;
+    __shared__ int32_t part[1024];
+    __shared__ int32_t base_count;
+    const int tid = threadIdx.x;
+    const int per = (E + 1023) / 1024;
+    const int lo = min(E, tid * per), hi = min(E, lo + per);
+    int32_t nd = 0;
+    for (int e = lo; e < hi; ++e) nd += trunc[e] ? 1 : 0;
+    part[tid] = nd;
+    if (tid == 0) base_count = *r.log_count;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int32_t v = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int32_t k = base_count + part[tid] - nd;
+    for (int e = lo; e < hi; ++e) {
+        const float rs = rsum[e];
+        const float d = trunc[e] ? 1.0f : 0.0f;
+        r.rewards[e] = rs * strength;
+        r.dones[e] = d;
+        r.timeouts[e] = d;
+        if (r.timeout_values) r.timeout_values[e] = tv_raw[e] * d;
+        float acc = r.episode_reward[e] + rs;
+        float steps = r.episode_steps[e] + dp;
+        if (trunc[e]) {
+            if (k < r.log_capacity) {
+                if (r.log_returns) r.log_returns[k] = acc;
+                if (r.log_lengths) r.log_lengths[k] = steps;
+                if (r.log_group_rewards) r.log_group_rewards[k] = group[e];
+            }
+            ++k;
+            acc = 0.0f;
+            steps = 0.0f;
+        }
+        r.episode_reward[e] = acc;
+        r.episode_steps[e] = steps;
+    }
+    __syncthreads();
+    if (tid == 1023) *r.log_count = base_count + part[1023];
+}
+
+// One workgroup per env: returns at once unless the env is done, then zeroes
+// its rows of every memory slab (actor / critic / baseline LSTM state).
+__global__ void __launch_bounds__(256) memory_reset_kernel(RecordArgs a, const uint8_t* __restrict__ trunc) {
+    const int e = blockIdx.x;
+    if (!trunc[e]) return;
+    const swarm_decision_record_t& r = a.r;
+    for (int m = 0; m < r.n_memories; ++m) {
+        const swarm_memory_slab_t s = r.memories[m];
+        const int64_t n = (int64_t)s.rows_per_env * s.width;
+        float* p = s.data + (int64_t)e * n;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0f;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int32_t swarm_decision_record(int32_t E, int32_t decision_period, double reward_strength, const float* reward_sum,
+                              const uint8_t* truncated, const float* timeout_value_raw,
+                              const float* completed_group_reward, const swarm_decision_record_t* rec,
+                              void* stream) {
+    if (E <= 0 || decision_period <= 0 || !rec || !reward_sum || !truncated || !completed_group_reward)
+        return SWARM_ERR_ARG;
+    if (!rec->rewards || !rec->dones || !rec->timeouts || !rec->episode_reward || !rec->episode_steps ||
+        !rec->log_count || rec->log_capacity < 0)
+        return SWARM_ERR_ARG;
+    if (rec->timeout_values && !timeout_value_raw) return SWARM_ERR_ARG;
+    if (rec->n_memories < 0 || rec->n_memories > SWARM_RECORD_MAX_MEMORIES) return SWARM_ERR_ARG;
+    for (int m = 0; m < rec->n_memories; ++m)
+        if (!rec->memories[m].data || rec->memories[m].rows_per_env <= 0 || rec->memories[m].width <= 0)
+            return SWARM_ERR_ARG;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    RecordArgs a{*rec};
+    // torch multiplies an fp32 tensor by a Python scalar rounded to fp32
+    record_kernel<<<1, 1024, 0, s>>>(a, E, (float)decision_period, (float)reward_strength, reward_sum, truncated,
+                                     timeout_value_raw, completed_group_reward);
+    if (rec->n_memories > 0) memory_reset_kernel<<<E, 256, 0, s>>>(a, truncated);
+    return swarm::record_hip_status();
+}
+
 
 int32_t swarm_lambda_returns(int32_t T, int32_t E, int32_t N, double gamma, double lam, const float* rewards,
                              const float* dones, const float* timeouts, const float* timeout_values,
@@ -313,7 +409,7 @@ int32_t swarm_sequence_chunk_offsets(int32_t T, int32_t E, int32_t N, int32_t L,
     // worst case: a done every step -> T windows per env
     if ((int64_t)T * E * N >= ((int64_t)1 << 31)) return SWARM_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (E > 0) chunk_count_kernel<<<(E + 255) / 256, 256, 0, s>>>(T, E, N, L, dones, env_offsets);
+    if (E > 0) chunk_count_kernel<<<(E + 63) / 64, 64, 0, s>>>(T, E, N, L, dones, env_offsets);
     exclusive_scan_kernel<<<1, 1024, 0, s>>>(E, env_offsets);
     return swarm::record_hip_status();
 }
@@ -324,7 +420,7 @@ int32_t swarm_sequence_chunk_fill(int32_t T, int32_t E, int32_t N, int32_t L, co
         return SWARM_ERR_ARG;
     if (E == 0 || T == 0) return SWARM_OK;
     hipStream_t s = static_cast<hipStream_t>(stream);
-    chunk_fill_kernel<<<(E + 255) / 256, 256, 0, s>>>(T, E, N, L, dones, env_offsets,
+    chunk_fill_kernel<<<(E + 63) / 64, 64, 0, s>>>(T, E, N, L, dones, env_offsets,
                                                      reinterpret_cast<int4*>(chunks));
     return swarm::record_hip_status();
 }

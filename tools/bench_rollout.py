@@ -107,12 +107,29 @@ def main():
             n_rows += b["obs"].shape[0]
         return n_rows
 
+    arrays = {a: getattr(buf, a) for _k, a, kind in spec if a}
+
+    def gathers():
+        """The device work of one epoch: chunk table, permutation, every window's
+        gather launch (no per-batch dict / view construction)."""
+        chunks, n = R.sequence_chunks(buf.dones[:T], N, L)
+        order = torch.randperm(n, device=dev)
+        per = max(1, args.batch // L)
+        starts = R.batch_starts(n, per)
+        per_window = max(1, (256 << 20) // (out_row * per))
+        for w in range(0, len(starts), per_window):
+            grp = starts[w:w + per_window]
+            R.gather(0, spec, arrays, order[grp[0]:min(grp[-1] + per, n)], chunks=chunks, n_items=n, L=L, T=T,
+                     E=E, N=N)
+        return len(starts) * per
+
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     rows = epoch()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    sec = timed(epoch, 2)
+    iter_sec = timed(epoch, 2)
+    sec = timed(gathers, 3)
     # algorithmic bytes: every output word written once and (except padding) read once
     algo = rows * out_row * 2
     # CPU: the reference's chunk enumeration + per-chunk slicing restated in numpy, on a sample of envs
@@ -126,12 +143,65 @@ def main():
         RO.gather_sequences(chunks, perm[a0:a0 + per], Lc, data_spec, cpu_arr)
     cpu_s = (time.perf_counter() - t0) * E / ce
     print(json.dumps({"stage": "sequence_batches_epoch", "ms": sec * 1e3, "first_epoch_wall_ms": wall * 1e3,
+                      "iterate_ms": iter_sec * 1e3,
+                      "note": "ms = device work of one epoch (chunk table + randperm + window gathers); iterate_ms "
+                              "adds building the per-batch dicts of views (host-bound, ~0.7 us per view)",
                       "rows": rows, "algorithmic_bytes": algo,
                       "roofline": {"bound": "hbm", "achieved": algo / sec / 1e9, "peak": PEAK, "unit": "GB/s",
                                    "frac": algo / sec / 1e9 / PEAK},
                       "cpu_baseline": {"ms": cpu_s * 1e3, "kind": "port", "cores": 1,
                                        "sample": f"oracle/rollout_oracle.py numpy, {ce} envs, scaled x{E / ce:g}"},
                       "config": cfg}), flush=True)
+    bench_record(E, N, H, dev)
+
+
+def bench_record(E, N, H, dev):
+    """Per-decision glue at C3 (cyclamen: recurrent actor + critic, 6 LSTM memory slabs)."""
+    from SwarmACB_isaac.agents import DecisionRecorder
+
+    rec = DecisionRecorder(E, dev, log_capacity=1 << 20)
+    row = {k: torch.zeros(E, device=dev) for k in ("rewards", "dones", "timeouts", "timeout_values")}
+    rs = torch.randn(E, device=dev).round()
+    tr = torch.zeros(E, dtype=torch.uint8, device=dev)
+    tr[::97] = 1
+    grp, tv = torch.randn(E, device=dev), torch.randn(E, device=dev)
+    mems = [(torch.randn(1, E * N, H // 2, device=dev), N), (torch.randn(1, E * N, H // 2, device=dev), N),
+            (torch.randn(1, E, H // 2, device=dev), 1), (torch.randn(1, E, H // 2, device=dev), 1),
+            (torch.randn(1, E * N, H // 2, device=dev), N), (torch.randn(1, E * N, H // 2, device=dev), N)]
+    sec = timed(lambda: rec.record(row, rs, tr, grp, 5, 1.0, timeout_value_raw=tv, memories=mems), 200)
+    rec.drain()
+
+    # the reference's per-decision ops on the same device (PT:575-634), for comparison
+    acc, cnt = torch.zeros(E, device=dev), torch.zeros(E, device=dev)
+    logs = []
+
+    def torch_glue():
+        last_done = torch.max(torch.zeros(E, device=dev), tr.bool().float())
+        last_timeout = torch.max(torch.zeros(E, device=dev), tr.bool().float())
+        row["timeout_values"].copy_(tv * last_timeout)
+        row["rewards"].copy_(rs * 1.0)
+        row["dones"].copy_(last_done)
+        row["timeouts"].copy_(last_timeout)
+        acc.add_(rs)
+        cnt.add_(5)
+        done_mask = last_done.bool()
+        if done_mask.any():
+            logs.extend(acc[done_mask].tolist())
+            logs.extend(cnt[done_mask].tolist())
+            logs.extend(grp[done_mask].tolist())
+            acc[done_mask] = 0.0
+            cnt[done_mask] = 0.0
+            da = done_mask[:, None].expand(E, N).reshape(-1)
+            for m, rows in mems:
+                m[:, da if rows == N else done_mask, :] = 0.0
+
+    ref_sec = timed(torch_glue, 50)
+    moved = E * (4 + 1 + 4 + 4 + 4 * 4 + 8)  # reads + writes per env of the record kernel
+    print(json.dumps({"stage": "decision_record", "ms": sec * 1e3, "torch_restatement_ms": ref_sec * 1e3,
+                      "algorithmic_bytes": moved,
+                      "note": "one decision's glue at C3 (8192 envs, 6 LSTM memory slabs, 1% of envs done); "
+                              "torch_restatement = the reference's per-decision ops incl. its done_mask host sync",
+                      "config": {"num_envs": E, "num_agents": N, "memory_size": H}}), flush=True)
 
 
 if __name__ == "__main__":

@@ -4,7 +4,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_rollout.py -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_rollout.py tests/test_gpu_glue.py -x -v --timeout 120 --timeout-method thread \
   > gpurun_out/pytest_rollout.log 2>&1
 RC=$?
 tail -30 gpurun_out/pytest_rollout.log
