@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
+    ap.add_argument("--critic", action="store_true",
+                    help="instead of the step: the fused critic attention at C3 (tools/bench_critic.py)")
     args, rest = ap.parse_known_args()
     args.rest = rest
     return args
@@ -106,12 +108,17 @@ def load_pmc(envs: int, sub: int) -> dict:
 
 def main():
     args = parse()
-    if args.rollout:
+    if args.rollout or args.critic:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import bench_rollout
-
         sys.argv = [sys.argv[0]] + args.rest
-        bench_rollout.main()
+        if args.rollout:
+            import bench_rollout
+
+            bench_rollout.main()
+        else:
+            import bench_critic
+
+            bench_critic.main()
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -1,0 +1,48 @@
+/*
+ * swarmcritic.h — C ABI of the fused critic attention kernel in libswarmstep.so.
+ *
+ * Trainer-side consumer of the e-puck step: the
+ * residual self-attention pooling of the centralised POCA critic, evaluated by
+ * all three trainers once per decision during rollout collection:
+ *
+ *   POCACritic.critic_pass        agents/poca_networks.py:629-645  (one set of N state entities)
+ *   POCACritic.joint_action_pass  agents/poca_networks.py:647-668  (one set of N state+action entities)
+ *   POCACritic.all_baselines      agents/poca_networks.py:822-882  (N counterfactual sets per env)
+ *   POCACritic.baseline           agents/poca_networks.py:764-788  (one set of 1 + M entities)
+ *   ResidualSelfAttention.forward agents/poca_networks.py:446-491  (the math of every set)
+ *
+ * Inputs are the DISTINCT entity rows of every env, already embedded and
+ * layer-normalised (x) and projected (qkv = x W_qkv^T + b_qkv); the kernel
+ * forms the entity sets itself, so the (B*N, N, h) set tensor of the reference
+ * is never materialised. Conventions as swarmstep.h: caller-owned device
+ * pointers, async on `stream`, 0 = ok, negative = swarm_status_t.
+ */
+#ifndef SWARMCRITIC_H
+#define SWARMCRITIC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    SWARM_RSA_SINGLE = 0,     /* one set per env: entities = rows 0 .. N-1 (R = N rows per env)      */
+    SWARM_RSA_BASELINES = 1   /* N sets per env (all_baselines): set i = [row i, rows N + j for j != i,
+                                 increasing j]; R = 2N rows per env: 0..N-1 state-only embeddings,
+                                 N..2N-1 state+action embeddings */
+} swarm_rsa_mode_t;
+
+/* pooled[(b * n_sets + s) * hidden + c] = mean over the N members of set s of
+ *   LayerNorm( fc_out( softmax_k(q k^T / sqrt(hidden)) v ) + x )[c]   (per head; no affine, eps 1e-5)
+ * x: [B][R][hidden] f32; qkv: [B][R][3*hidden] f32 (q | k | v); w_out: [hidden][hidden] (torch Linear
+ * layout, out x in); b_out: [hidden]; n_sets = 1 (SINGLE) or N (BASELINES).
+ * Supported: hidden = 128, heads in {1, 2, 4}, 1 <= N <= 20. fc_out runs on the matrix cores
+ * (v_mfma_f32_16x16x4_f32: exact fp32 products). x, qkv and pooled must be 16-byte aligned. */
+int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,
+                       const float* qkv, const float* w_out, const float* b_out, float* pooled, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWARMCRITIC_H */

@@ -66,6 +66,10 @@ class GatherField(C.Structure):
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("row_words", C.c_int32), ("kind", C.c_int32)]
 
 
+# Every symbol include/swarmcritic.h declares (fused critic attention, same library).
+CRITIC_EXPORTS = ["swarm_rsa_pool"]
+RSA_SINGLE, RSA_BASELINES = 0, 1
+
 RECORD_MAX_MEMORIES = 8
 
 
@@ -127,6 +131,8 @@ def load() -> C.CDLL:
     lib.swarm_gather.argtypes = [i32, C.POINTER(GatherField), i32, vp, vp, i32, i32, i32, i32, i32, i64, vp, vp, vp]
     lib.swarm_decision_record.restype = i32
     lib.swarm_decision_record.argtypes = [i32, i32, C.c_double, vp, vp, vp, vp, C.POINTER(DecisionRecord), vp]
+    lib.swarm_rsa_pool.restype = i32
+    lib.swarm_rsa_pool.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -1,0 +1,405 @@
+"""MA-POCA actor / critic networks (drop-in for agents/poca_networks.py).
+
+The module tree, parameter names and initialisation order follow the
+reference (poca_networks.py:58-882), so its state_dicts and checkpoints load
+into these classes unchanged and a seeded construction draws the same weights.
+
+What is MI355X-specific is the critic's rollout-time evaluation: under
+``torch.no_grad()`` on the GPU (how all three trainers call ``critic_pass``,
+``joint_action_pass``, ``baseline`` and ``all_baselines`` once per decision),
+the residual self-attention runs as the fused HIP kernel of
+include/swarmcritic.h. The entity rows of an env are embedded, normalised and
+projected once (2N rows instead of the reference's N x N set rows), the
+kernel forms every counterfactual set itself and runs fc_out on the matrix
+cores. With autograd enabled (the PPO update) the PyTorch path below runs;
+it restates the reference math operation by operation.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+import torch.nn as nn
+from torch.distributions import Normal
+
+from .. import _native
+
+Swish = nn.SiLU  # ML-Agents' Swish
+
+_KERNEL_INITS = {
+    "kaiming_normal": lambda w: nn.init.kaiming_normal_(w, nonlinearity="linear"),
+    "normal": nn.init.normal_,
+    "xavier_uniform": nn.init.xavier_uniform_,
+}
+
+
+def _linear_layer(input_size: int, output_size: int, kernel_init: str = "xavier_uniform",
+                  kernel_gain: float = 1.0, bias_init: str = "zeros") -> nn.Linear:
+    """ML-Agents-initialised linear layer (poca_networks.py:58-82)."""
+    if kernel_init not in _KERNEL_INITS:
+        raise ValueError(f"Unknown kernel_init: {kernel_init}")
+    layer = nn.Linear(input_size, output_size)
+    _KERNEL_INITS[kernel_init](layer.weight)
+    layer.weight.data *= kernel_gain
+    if bias_init == "zeros":
+        nn.init.zeros_(layer.bias)
+    return layer
+
+
+def _mlagents_lstm(input_size: int, memory_size: int, forget_bias: float = 1.0) -> tuple[nn.LSTM, int]:
+    """LSTM with ML-Agents' memory convention (poca_networks.py:85-113): a memory
+    vector of `memory_size` holds h and c, i.e. memory_size // 2 units; Xavier per
+    gate block, forget-gate bias added to both bias tensors."""
+    memory_size = int(memory_size)
+    if memory_size <= 0 or memory_size % 2:
+        raise ValueError("ML-Agents memory_size must be a positive even integer")
+    units = memory_size // 2
+    lstm = nn.LSTM(input_size, units, batch_first=True)
+    for name, param in lstm.named_parameters():
+        gates = param.data.view(4, param.shape[0] // 4, *param.shape[1:])
+        if "weight" in name:
+            for g in range(4):
+                nn.init.xavier_uniform_(gates[g])
+        elif "bias" in name:
+            nn.init.zeros_(param)
+            gates[1].add_(forget_bias)
+    return lstm, units
+
+
+def checkpoint_memory_size(checkpoint: dict, default: int = 128) -> int:
+    """Total ML-Agents memory size of a checkpoint (poca_networks.py:116-127):
+    checkpoints older than the parity revision stored the LSTM unit count."""
+    value = int(checkpoint.get("memory_size", default))
+    return value if checkpoint.get("memory_size_semantics") == "mlagents_total" else 2 * value
+
+
+def _mlp(input_size: int, num_layers: int, hidden: int, kernel_init: str, kernel_gain: float = 1.0):
+    dims = [input_size] + [hidden] * num_layers
+    mods: list[nn.Module] = []
+    for a, b in zip(dims[:-1], dims[1:]):
+        mods += [_linear_layer(a, b, kernel_init=kernel_init, kernel_gain=kernel_gain), Swish()]
+    return nn.Sequential(*mods)
+
+
+class LinearEncoder(nn.Module):
+    """Linear + Swish stack (poca_networks.py:133-170)."""
+
+    def __init__(self, input_size: int, num_layers: int, hidden_size: int, kernel_init: str = "kaiming_normal",
+                 kernel_gain: float = 1.0):
+        super().__init__()
+        self.net = _mlp(input_size, num_layers, hidden_size, kernel_init, kernel_gain)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.net(x)
+
+
+class EntityEmbedding(nn.Module):
+    """One-layer entity encoder with T-Fixup init (poca_networks.py:173-194)."""
+
+    def __init__(self, entity_size: int, embedding_size: int):
+        super().__init__()
+        self.encoder = LinearEncoder(entity_size, 1, embedding_size, kernel_init="normal",
+                                     kernel_gain=(0.125 / embedding_size) ** 0.5)
+
+    def forward(self, entities: torch.Tensor) -> torch.Tensor:
+        return self.encoder(entities)
+
+
+class Actor(nn.Module):
+    """Gaussian actor, state-independent log-std, per-dimension log-probs
+    (poca_networks.py:197-257)."""
+
+    def __init__(self, obs_dim: int, act_dim: int, hidden: int = 256, num_layers: int = 2):
+        super().__init__()
+        self.net = _mlp(obs_dim, num_layers, hidden, "kaiming_normal")
+        self.mu_head = _linear_layer(hidden, act_dim, kernel_init="kaiming_normal", kernel_gain=0.2)
+        self.log_std = nn.Parameter(torch.zeros(1, act_dim))
+
+    def forward(self, obs: torch.Tensor):
+        mu = self.mu_head(self.net(obs))
+        return mu, (mu * 0 + self.log_std).exp()
+
+    def get_dist(self, obs: torch.Tensor) -> Normal:
+        return Normal(*self(obs))
+
+    def evaluate(self, obs: torch.Tensor, actions: torch.Tensor):
+        dist = self.get_dist(obs)
+        return dist.log_prob(actions), dist.entropy().mean(dim=-1)
+
+
+class DiscreteActor(nn.Module):
+    """Categorical actor over behaviour modules (poca_networks.py:260-314)."""
+
+    def __init__(self, obs_dim: int, num_actions: int, hidden: int = 256, num_layers: int = 2):
+        super().__init__()
+        self.num_actions = num_actions
+        self.net = _mlp(obs_dim, num_layers, hidden, "kaiming_normal")
+        self.logits_head = _linear_layer(hidden, num_actions, kernel_init="kaiming_normal", kernel_gain=0.1)
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        return self.logits_head(self.net(obs))
+
+    def get_dist(self, obs: torch.Tensor) -> torch.distributions.Categorical:
+        return torch.distributions.Categorical(logits=self(obs))
+
+    def evaluate(self, obs: torch.Tensor, actions: torch.Tensor):
+        dist = self.get_dist(obs)
+        return dist.log_prob(actions.squeeze(-1).long()).unsqueeze(-1), dist.entropy()
+
+
+class RecurrentDiscreteActor(nn.Module):
+    """Categorical actor with an LSTM memory, the cyclamen policy (poca_networks.py:320-414)."""
+
+    def __init__(self, obs_dim: int, num_actions: int, hidden: int = 128, num_layers: int = 1,
+                 memory_size: int = 128):
+        super().__init__()
+        self.obs_dim, self.num_actions, self.memory_size = obs_dim, num_actions, memory_size
+        self.net = LinearEncoder(obs_dim, num_layers, hidden, kernel_init="kaiming_normal")
+        self.lstm, self.hidden_size = _mlagents_lstm(hidden, memory_size)
+        self.logits_head = _linear_layer(self.hidden_size, num_actions, kernel_init="kaiming_normal",
+                                         kernel_gain=0.1)
+
+    def initial_state(self, batch_size: int, device):
+        z = torch.zeros(1, batch_size, self.hidden_size, device=device)
+        return z, z.clone()
+
+    def forward_sequence(self, obs_seq: torch.Tensor, state=None):
+        B, T = obs_seq.shape[:2]
+        enc = self.net(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
+        out, nxt = self.lstm(enc, state if state is not None else self.initial_state(B, obs_seq.device))
+        return self.logits_head(out), nxt
+
+    def step(self, obs: torch.Tensor, state=None):
+        logits, nxt = self.forward_sequence(obs.unsqueeze(1), state)
+        return logits[:, 0], nxt
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        return self.step(obs)[0]
+
+    def get_dist(self, obs: torch.Tensor, state=None) -> torch.distributions.Categorical:
+        return torch.distributions.Categorical(logits=self.step(obs, state)[0])
+
+    def evaluate_sequence(self, obs_seq: torch.Tensor, actions_seq: torch.Tensor, state=None):
+        B, T = obs_seq.shape[:2]
+        logits, _ = self.forward_sequence(obs_seq, state)
+        dist = torch.distributions.Categorical(logits=logits.reshape(B * T, self.num_actions))
+        act = actions_seq.reshape(B * T, -1).squeeze(-1).long()
+        return dist.log_prob(act).view(B, T, 1), dist.entropy().view(B, T)
+
+    def evaluate(self, obs: torch.Tensor, actions: torch.Tensor):
+        lp, ent = self.evaluate_sequence(obs.unsqueeze(1), actions.unsqueeze(1))
+        return lp[:, 0], ent[:, 0]
+
+
+class ResidualSelfAttention(nn.Module):
+    """Pre-norm multi-head self-attention + residual + masked mean pooling
+    (poca_networks.py:417-491); LayerNorms without affine parameters, logits
+    scaled by sqrt(embed_dim)."""
+
+    NEG_INF = -1e6
+    EPSILON = 1e-7
+
+    def __init__(self, embed_dim: int, num_heads: int = 4):
+        super().__init__()
+        assert embed_dim % num_heads == 0
+        self.num_heads, self.head_dim, self.embed_dim = num_heads, embed_dim // num_heads, embed_dim
+        gain = (0.125 / embed_dim) ** 0.5
+        for name in ("fc_q", "fc_k", "fc_v", "fc_out"):
+            setattr(self, name, _linear_layer(embed_dim, embed_dim, kernel_init="normal", kernel_gain=gain))
+        self.embedding_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
+        self.residual_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
+
+    def forward(self, inp: torch.Tensor, key_mask: torch.Tensor | None = None) -> torch.Tensor:
+        B, N, D = inp.shape
+        H, d = self.num_heads, self.head_dim
+        x = self.embedding_norm(inp)
+        heads = [f(x).view(B, N, H, d).transpose(1, 2) for f in (self.fc_q, self.fc_k, self.fc_v)]
+        logits = (heads[0] @ heads[1].transpose(-2, -1)) / math.sqrt(D)
+        if key_mask is not None:
+            logits = logits + key_mask.view(B, 1, 1, N) * self.NEG_INF
+        att = (logits.softmax(dim=-1) @ heads[2]).transpose(1, 2).contiguous().view(B, N, D)
+        out = self.residual_norm(self.fc_out(att) + x)
+        if key_mask is None:
+            return out.mean(dim=1)
+        keep = (1.0 - key_mask).unsqueeze(-1)
+        return (out * keep).sum(dim=1) / (keep.sum(dim=1) + self.EPSILON)
+
+
+def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode: int, n: int) -> torch.Tensor:
+    """Attention pooling of the entity sets of every env through swarm_rsa_pool.
+    rows: (B, R, h) embedded entities (R = n, or 2n for the baseline sets)."""
+    B = rows.shape[0]
+    x = attn.embedding_norm(rows).contiguous()
+    w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
+    b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
+    qkv = torch.nn.functional.linear(x, w, b).contiguous()
+    n_sets = n if mode == _native.RSA_BASELINES else 1
+    pooled = torch.empty(B * n_sets, attn.embed_dim, dtype=torch.float32, device=rows.device)
+    wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
+    lib = _native.load()
+    rc = lib.swarm_rsa_pool(mode, B, n, attn.num_heads, attn.embed_dim, C.c_void_p(x.data_ptr()),
+                            C.c_void_p(qkv.data_ptr()), C.c_void_p(wo.data_ptr()), C.c_void_p(bo.data_ptr()),
+                            C.c_void_p(pooled.data_ptr()),
+                            C.c_void_p(torch.cuda.current_stream(rows.device).cuda_stream))
+    _native.check(rc, "swarm_rsa_pool")
+    return pooled
+
+
+class POCACritic(nn.Module):
+    """Centralised attention critic over the 5-D polar agent states with
+    counterfactual baselines (poca_networks.py:506-882)."""
+
+    FUSED_HIDDEN = 128
+    FUSED_HEADS = (1, 2, 4)
+    FUSED_MAX_ENTITIES = 20
+
+    def __init__(self, state_dim: int, act_dim: int, num_agents: int, h_size: int = 256, num_heads: int = 4,
+                 num_layers: int = 2, memory_size: int = 0):
+        super().__init__()
+        self.state_dim, self.act_dim, self.num_agents, self.h_size = state_dim, act_dim, num_agents, h_size
+        self.memory_size = int(memory_size or 0)
+        self.obs_entity_enc = EntityEmbedding(state_dim, h_size)
+        self.obs_act_entity_enc = EntityEmbedding(state_dim + act_dim, h_size)
+        self.self_attn = ResidualSelfAttention(h_size, num_heads)
+        self.linear_encoder = LinearEncoder(h_size, num_layers, h_size, kernel_init="kaiming_normal",
+                                            kernel_gain=(0.125 / h_size) ** 0.5)
+        if self.memory_size > 0:
+            self.lstm, self.hidden_size = _mlagents_lstm(h_size, self.memory_size)
+        else:
+            self.lstm, self.hidden_size = None, h_size
+        self.value_head = _linear_layer(self.hidden_size + 1, 1, kernel_init="xavier_uniform")
+        self._current_max_agents = nn.Parameter(torch.tensor(1.0), requires_grad=False)
+        self.use_fused = True  # set False to force the PyTorch path (benchmarks, debugging)
+
+    # ------------------------------------------------------------ helpers
+    def _norm_agent_count(self, n: int, B: int, device) -> torch.Tensor:
+        """n in [-1, 1] against the largest n seen (poca_networks.py:579-584)."""
+        if n > self._current_max_agents.item():
+            self._current_max_agents.data.fill_(float(n))
+        return torch.full((B, 1), n * 2.0 / self._current_max_agents.item() - 1.0, device=device)
+
+    def initial_state(self, batch_size: int, device):
+        if self.lstm is None:
+            return None
+        z = torch.zeros(1, batch_size, self.hidden_size, device=device)
+        return z, z.clone()
+
+    def _fused(self, ref: torch.Tensor, n_entities: int) -> bool:
+        return (self.use_fused and ref.is_cuda and not torch.is_grad_enabled()
+                and self.h_size == self.FUSED_HIDDEN and self.self_attn.num_heads in self.FUSED_HEADS
+                and 1 <= n_entities <= self.FUSED_MAX_ENTITIES)
+
+    def _value_tail(self, pooled, n_agents, memory=None, sequence_length=1, return_memory=False):
+        """linear encoder -> [LSTM] -> agent count -> value head (poca_networks.py:608-625)."""
+        B = pooled.shape[0]
+        encoding = self.linear_encoder(pooled)
+        next_memory = memory
+        if self.lstm is not None:
+            sequence_length = int(sequence_length)
+            if sequence_length <= 0 or B % sequence_length:
+                raise ValueError("Critic batch must be divisible by sequence_length")
+            n_seq = B // sequence_length
+            seq, next_memory = self.lstm(encoding.view(n_seq, sequence_length, self.h_size),
+                                         memory if memory is not None else self.initial_state(n_seq, encoding.device))
+            encoding = seq.reshape(B, self.hidden_size)
+        encoding = torch.cat([encoding, self._norm_agent_count(n_agents, B, encoding.device)], dim=-1)
+        value = self.value_head(encoding)
+        return (value, next_memory) if return_memory else value
+
+    def _encode_and_value(self, entities, n_agents, memory=None, sequence_length=1, return_memory=False):
+        """RSA -> tail on explicit entity sets (B, n, h) (poca_networks.py:597-625)."""
+        if self._fused(entities, entities.shape[1]):
+            pooled = _fused_rsa(self.self_attn, entities, _native.RSA_SINGLE, entities.shape[1])
+        else:
+            pooled = self.self_attn(entities)
+        return self._value_tail(pooled, n_agents, memory, sequence_length, return_memory)
+
+    # ------------------------------------------------------------ public API
+    def critic_pass(self, all_agent_states, memory=None, sequence_length: int = 1, return_memory: bool = False):
+        """V(s) from the state-only entities of all agents (poca_networks.py:629-645)."""
+        N = all_agent_states.shape[1]
+        return self._encode_and_value(self.obs_entity_enc(all_agent_states), N, memory, sequence_length,
+                                      return_memory)
+
+    def joint_action_pass(self, all_agent_states, all_agent_actions, memory=None, sequence_length: int = 1,
+                          return_memory: bool = False):
+        """Q(s, a) over state+action entities (poca_networks.py:647-668)."""
+        N = all_agent_states.shape[1]
+        ents = self.obs_act_entity_enc(torch.cat([all_agent_states, all_agent_actions], dim=-1))
+        return self._encode_and_value(ents, N, memory, sequence_length, return_memory)
+
+    def all_discrete_counterfactual_values(self, all_agent_states, action_indices, num_actions: int):
+        """Q for every discrete alternative of every agent, peers fixed (poca_networks.py:670-713)."""
+        B, N, _ = all_agent_states.shape
+        alts = torch.arange(num_actions, device=all_agent_states.device)
+        states = all_agent_states.unsqueeze(1).expand(B, num_actions, N, self.state_dim).reshape(
+            B * num_actions, N, self.state_dim)
+        out = []
+        for agent in range(N):
+            idx = action_indices.unsqueeze(1).expand(B, num_actions, N).clone()
+            idx[:, :, agent] = alts.unsqueeze(0)
+            onehot = torch.nn.functional.one_hot(idx.reshape(B * num_actions, N).long(),
+                                                 num_classes=num_actions).to(all_agent_states.dtype)
+            out.append(self.joint_action_pass(states, onehot).reshape(B, num_actions))
+        return torch.stack(out, dim=1)
+
+    def focal_discrete_counterfactual_values(self, all_agent_states, action_indices, focal_agent_ids,
+                                             num_actions: int, memory=None):
+        """Q for every alternative of one focal agent per row (poca_networks.py:715-762)."""
+        B, N, _ = all_agent_states.shape
+        dev = all_agent_states.device
+        idx = action_indices.unsqueeze(1).expand(B, num_actions, N).clone()
+        idx[torch.arange(B, device=dev).unsqueeze(1), torch.arange(num_actions, device=dev).unsqueeze(0),
+            focal_agent_ids.long().unsqueeze(1).expand(-1, num_actions)] = \
+            torch.arange(num_actions, device=dev).unsqueeze(0)
+        onehot = torch.nn.functional.one_hot(idx.reshape(B * num_actions, N).long(),
+                                             num_classes=num_actions).to(all_agent_states.dtype)
+        states = all_agent_states.unsqueeze(1).expand(B, num_actions, N, self.state_dim).reshape(
+            B * num_actions, N, self.state_dim)
+        mem = None
+        if memory is not None:
+            mem = tuple(m.unsqueeze(2).expand(-1, -1, num_actions, -1).reshape(m.shape[0], B * num_actions,
+                                                                               m.shape[-1]) for m in memory)
+        return self.joint_action_pass(states, onehot, memory=mem).reshape(B, num_actions)
+
+    def baseline(self, agent_i_state, other_states, other_actions, memory=None, sequence_length: int = 1,
+                 return_memory: bool = False):
+        """Counterfactual b_i: agent i state-only, the others state+action (poca_networks.py:764-788)."""
+        M = other_states.shape[1]
+        ents = torch.cat([self.obs_entity_enc(agent_i_state.unsqueeze(1)),
+                          self.obs_act_entity_enc(torch.cat([other_states, other_actions], dim=-1))], dim=1)
+        return self._encode_and_value(ents, 1 + M, memory, sequence_length, return_memory)
+
+    def focal_baselines(self, all_states, all_actions, focal_agent_ids, memory=None, sequence_length: int = 1,
+                        return_memory: bool = False):
+        """One baseline per row for its focal agent (poca_networks.py:790-820)."""
+        B, N, _ = all_states.shape
+        rows = torch.arange(B, device=all_states.device)
+        focal = focal_agent_ids.long()
+        keep = torch.ones(B, N, dtype=torch.bool, device=all_states.device)
+        keep[rows, focal] = False
+        return self.baseline(all_states[rows, focal], all_states[keep].view(B, N - 1, self.state_dim),
+                             all_actions[keep].view(B, N - 1, self.act_dim), memory, sequence_length,
+                             return_memory)
+
+    def all_baselines(self, all_states, all_actions, memory=None, sequence_length: int = 1,
+                      return_memory: bool = False):
+        """Baselines of every agent in one pass (poca_networks.py:822-882): set (b, i)
+        = [state-only entity i, state+action entities j != i in increasing j]."""
+        B, N, _ = all_states.shape
+        obs_emb = self.obs_entity_enc(all_states)
+        act_emb = self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1))
+        if self._fused(all_states, N):
+            pooled = _fused_rsa(self.self_attn, torch.cat([obs_emb, act_emb], dim=1), _native.RSA_BASELINES, N)
+        else:
+            others = ~torch.eye(N, dtype=torch.bool, device=all_states.device)
+            peers = act_emb.unsqueeze(1).expand(B, N, N, self.h_size)[:, others].view(B, N, N - 1, self.h_size)
+            sets = torch.cat([obs_emb.unsqueeze(2), peers], dim=2).reshape(B * N, N, self.h_size)
+            pooled = self.self_attn(sets)
+        result = self._value_tail(pooled, N, memory, sequence_length, return_memory)
+        if return_memory:
+            values, next_memory = result
+            return values.squeeze(-1).reshape(B, N), next_memory
+        return result.squeeze(-1).reshape(B, N)

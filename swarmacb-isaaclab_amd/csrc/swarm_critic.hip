@@ -1,0 +1,273 @@
+// swarm_critic.hip — fused residual-self-attention pooling of the centralised
+// POCA critic for gfx950. C ABI: include/swarmcritic.h.
+//
+// Reference: poca_networks.py ResidualSelfAttention.forward (:446-491) as used
+// by POCACritic.critic_pass / joint_action_pass / baseline / all_baselines
+// (:629-882). For all_baselines the reference materialises, for every env b
+// and agent i, the entity set [state embedding of i, state+action embeddings
+// of every j != i] as a (B*N, N, h) tensor and runs LayerNorm, three h x h
+// projections, attention, fc_out, LayerNorm and a mean over every set row.
+//
+// Here the per-entity work is done once per env instead of once per set: the
+// host projects the 2N distinct entity rows (x = LN(embedding), qkv = x W^T,
+// one library GEMM), and this kernel
+//   phase 0  stages x, q, k, v of one env in LDS;
+//   phase 1  computes the attention logits of every entity pair and head
+//            (all sets of the env share them);
+//   phase 2  walks the sets four at a time (one per wave): softmax + P.V on the
+//            VALU, then fc_out for the chunk's 4N rows on the matrix cores
+//            (v_mfma_f32_16x16x4_f32, exact fp32 products; W_out is held in
+//            VGPRs as B fragments for the whole persistent kernel), bias +
+//            residual, LayerNorm and the mean over the set, written as pooled.
+// One persistent workgroup per CU (4 waves, ~149 KiB of LDS) walks the envs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/swarmcritic.h"
+#include "../../include/swarmstep.h"
+#include "swarm_launch.h"
+
+namespace {
+
+constexpr int HD = 128;           // embedding width (critic hidden_units of the cyclamen / tulip / OC configs)
+constexpr int NMAX = 20;          // entities per set
+constexpr int RMAX = 2 * NMAX;    // entity rows per env
+constexpr int SETS = 4;           // sets per chunk: one per wave
+constexpr int LDSW = HD + 4;      // padded LDS row stride
+constexpr int CROWS = SETS * NMAX;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// entity row of member k of set s (swarm_rsa_mode_t)
+__device__ __forceinline__ int member(int mode, int N, int s, int k) {
+    if (mode == SWARM_RSA_SINGLE) return k;
+    return k == 0 ? s : N + (k - 1 < s ? k - 1 : k);
+}
+
+template <int NH>
+__global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, const float* __restrict__ X,
+                                                       const float* __restrict__ QKV, const float* __restrict__ Wo,
+                                                       const float* __restrict__ bo, float* __restrict__ pooled) {
+    constexpr int DH = HD / NH;   // head width
+    constexpr int CW = DH / 4;    // output channels per P.V work item
+    const int R = mode == SWARM_RSA_SINGLE ? N : 2 * N;
+    const int n_sets = mode == SWARM_RSA_SINGLE ? 1 : N;
+
+    __shared__ float Xs[RMAX * LDSW];
+    __shared__ float Vs[RMAX * LDSW];
+    __shared__ float S[NH * RMAX * RMAX];
+    __shared__ float QKO[CROWS * LDSW];  // q | k rows (phases 0-1), then the chunk's attention outputs
+    __shared__ float PF[CROWS * LDSW];   // softmax probabilities (2a), then the chunk's fc_out rows (2b-2c)
+    float* Qs = QKO;
+    float* Ks = QKO + RMAX * LDSW;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int q = lane >> 4;      // MFMA k-group of this lane
+
+    // W_out^T as MFMA B fragments for this wave's 32 output columns, resident for
+    // the whole kernel. The k order is permuted (same permutation on the A side):
+    // k-step ks of lane group q is input feature k = 32 q + ks, so each lane reads
+    // its A operands as 8 contiguous float4s of a row.
+    float b0[HD / 4], b1[HD / 4];
+    {
+        const float* w0 = Wo + (32 * wave + (lane & 15)) * HD + 32 * q;
+        const float* w1 = w0 + 16 * HD;
+#pragma unroll
+        for (int ks = 0; ks < HD / 4; ++ks) {
+            b0[ks] = w0[ks];
+            b1[ks] = w1[ks];
+        }
+    }
+    const float sqrt_d = 11.313708498984761f;  // torch divides the logits by math.sqrt(h)
+
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+        // ---- phase 0: x, q, k, v rows of this env
+        const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)b * R * HD);
+        const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)b * R * 3 * HD);
+        for (int i = tid; i < R * (HD / 4); i += 256) {
+            const int r = i / (HD / 4), c = 4 * (i % (HD / 4));
+            *reinterpret_cast<float4*>(&Xs[r * LDSW + c]) = x4[i];
+        }
+        for (int i = tid; i < R * (3 * HD / 4); i += 256) {
+            const int r = i / (3 * HD / 4), c = 4 * (i % (3 * HD / 4));
+            float* dst = c < HD ? &Qs[r * LDSW + c] : c < 2 * HD ? &Ks[r * LDSW + c - HD] : &Vs[r * LDSW + c - 2 * HD];
+            *reinterpret_cast<float4*>(dst) = q4[i];
+        }
+        __syncthreads();
+        // ---- phase 1: logits of every entity pair and head
+        for (int e = tid; e < NH * R * R; e += 256) {
+            const int h = e / (R * R);
+            const int rem = e - h * R * R;
+            const int qr = rem / R, kr = rem - (rem / R) * R;
+            const float* qp = &Qs[qr * LDSW + h * DH];
+            const float* kp = &Ks[kr * LDSW + h * DH];
+            float acc = 0.0f;
+#pragma unroll
+            for (int d = 0; d < DH; d += 4) {
+                const float4 u = *reinterpret_cast<const float4*>(qp + d);
+                const float4 v = *reinterpret_cast<const float4*>(kp + d);
+                acc += u.x * v.x;
+                acc += u.y * v.y;
+                acc += u.z * v.z;
+                acc += u.w * v.w;
+            }
+            S[(h * RMAX + qr) * RMAX + kr] = acc / sqrt_d;
+        }
+        __syncthreads();
+        // ---- phase 2: sets in chunks of SETS (wave w owns set s0 + w)
+        for (int s0 = 0; s0 < n_sets; s0 += SETS) {
+            const int set = s0 + wave;
+            const bool have = set < n_sets;
+            float* P = &PF[wave * NH * NMAX * NMAX];
+            // 2a-1: softmax over the set's members for every (row, head)
+            if (have) {
+                for (int p = lane; p < N * NH; p += 64) {
+                    const int r = p / NH, h = p - (p / NH) * NH;
+                    const float* srow = &S[(h * RMAX + member(mode, N, set, r)) * RMAX];
+                    float l[NMAX];
+                    float m = -INFINITY;
+#pragma unroll
+                    for (int k = 0; k < NMAX; ++k)
+                        if (k < N) {
+                            l[k] = srow[member(mode, N, set, k)];
+                            m = fmaxf(m, l[k]);
+                        }
+                    float sum = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < NMAX; ++k)
+                        if (k < N) {
+                            l[k] = expf(l[k] - m);
+                            sum += l[k];
+                        }
+                    float* prow = &P[(h * NMAX + r) * NMAX];
+#pragma unroll
+                    for (int k = 0; k < NMAX; ++k)
+                        if (k < N) prow[k] = l[k] / sum;
+                }
+            }
+            __syncthreads();
+            // 2a-2: attention outputs O[row][h*DH + c] = sum_k P[h][row][k] v[member k][h*DH + c]
+            if (have) {
+                for (int it = lane; it < N * NH * 4; it += 64) {
+                    const int r = it / (NH * 4);
+                    const int rem = it - r * (NH * 4);
+                    const int h = rem >> 2, c0 = h * DH + (rem & 3) * CW;
+                    const float* prow = &P[(h * NMAX + r) * NMAX];
+                    float4 o[CW / 4];
+#pragma unroll
+                    for (int c = 0; c < CW / 4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int k = 0; k < NMAX; ++k)
+                        if (k < N) {
+                            const float pk = prow[k];
+                            const float* vrow = &Vs[member(mode, N, set, k) * LDSW + c0];
+#pragma unroll
+                            for (int c = 0; c < CW / 4; ++c) {
+                                const float4 v = *reinterpret_cast<const float4*>(vrow + 4 * c);
+                                o[c].x += pk * v.x;
+                                o[c].y += pk * v.y;
+                                o[c].z += pk * v.z;
+                                o[c].w += pk * v.w;
+                            }
+                        }
+                    float* orow = &QKO[(wave * N + r) * LDSW + c0];
+#pragma unroll
+                    for (int c = 0; c < CW / 4; ++c) *reinterpret_cast<float4*>(orow + 4 * c) = o[c];
+                }
+            }
+            __syncthreads();
+            // 2b: fc_out on the matrix cores. Rows = the chunk's set rows (16-row tiles),
+            // this wave's 32 columns as two 16-column tiles sharing the A operand.
+            const int rows = min(SETS, n_sets - s0) * N;
+            const int mtiles = (rows + 15) >> 4;
+            for (int mt = 0; mt < mtiles; ++mt) {
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                const float* arow = &QKO[(mt * 16 + (lane & 15)) * LDSW + 32 * q];
+#pragma unroll
+                for (int m = 0; m < HD / 16; ++m) {
+                    const float4 a = *reinterpret_cast<const float4*>(arow + 4 * m);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0[4 * m + 0], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b1[4 * m + 0], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0[4 * m + 1], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1[4 * m + 1], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0[4 * m + 2], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b1[4 * m + 2], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0[4 * m + 3], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b1[4 * m + 3], acc1, 0, 0, 0);
+                }
+                // D layout: column lane & 15, rows 4 (lane >> 4) + i
+                const int col0 = 32 * wave + (lane & 15), col1 = col0 + 16;
+                const float bias0 = bo[col0], bias1 = bo[col1];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = mt * 16 + 4 * q + i;
+                    if (row < rows) {
+                        const int sl = row / N, r = row - sl * N;
+                        const float* xr = &Xs[member(mode, N, s0 + sl, r) * LDSW];
+                        PF[row * LDSW + col0] = (acc0[i] + bias0) + xr[col0];
+                        PF[row * LDSW + col1] = (acc1[i] + bias1) + xr[col1];
+                    }
+                }
+            }
+            __syncthreads();
+            // 2c: LayerNorm (no affine, eps 1e-5) of every row of this wave's set, mean over the set
+            if (have) {
+                float p0 = 0.0f, p1 = 0.0f;
+                for (int r = 0; r < N; ++r) {
+                    const float2 f = *reinterpret_cast<const float2*>(&PF[(wave * N + r) * LDSW + 2 * lane]);
+                    const float mean = wave_sum(f.x + f.y) * (1.0f / HD);
+                    const float d0 = f.x - mean, d1 = f.y - mean;
+                    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / HD);
+                    const float rstd = 1.0f / sqrtf(var + 1e-5f);
+                    p0 += d0 * rstd;
+                    p1 += d1 * rstd;
+                }
+                *reinterpret_cast<float2*>(&pooled[((size_t)b * n_sets + set) * HD + 2 * lane]) =
+                    make_float2(p0 / (float)N, p1 / (float)N);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+int g_cus = 0;
+
+}  // namespace
+
+extern "C" {
+
+int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,
+                       const float* qkv, const float* w_out, const float* b_out, float* pooled, void* stream) {
+    if (mode != SWARM_RSA_SINGLE && mode != SWARM_RSA_BASELINES) return SWARM_ERR_ARG;
+    if (hidden != HD || B < 0 || N < 1 || N > NMAX) return SWARM_ERR_ARG;
+    if (heads != 1 && heads != 2 && heads != 4) return SWARM_ERR_ARG;
+    if (B == 0) return SWARM_OK;
+    if (!x || !qkv || !w_out || !b_out || !pooled) return SWARM_ERR_ARG;
+    if ((((uintptr_t)x) | ((uintptr_t)qkv) | ((uintptr_t)pooled)) & 15) return SWARM_ERR_ARG;
+    if (g_cus == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        g_cus = cus;
+    }
+    const int grid = B < g_cus ? B : g_cus;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (heads == 1)
+        rsa_pool_kernel<1><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+    else if (heads == 2)
+        rsa_pool_kernel<2><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+    else
+        rsa_pool_kernel<4><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+    return swarm::record_hip_status();
+}
+
+}  // extern "C"

@@ -12,7 +12,8 @@ from conftest import ROOT
 from SwarmACB_isaac import _native
 from SwarmACB_isaac.engine import fsm_pack, fsm_unpack
 
-HEADERS = {"swarmstep.h": _native.EXPORTS, "swarmrollout.h": _native.ROLLOUT_EXPORTS}
+HEADERS = {"swarmstep.h": _native.EXPORTS, "swarmrollout.h": _native.ROLLOUT_EXPORTS,
+           "swarmcritic.h": _native.CRITIC_EXPORTS}
 
 
 def declared_functions(header: str = "swarmstep.h") -> list[str]:

@@ -1,0 +1,120 @@
+"""GPU parity of the fused critic attention (swarm_rsa_pool, include/swarmcritic.h)
+as used by the drop-in POCACritic under torch.no_grad() on the GPU.
+
+Against (1) the reference modules' own outputs (tests/golden/critic/
+poca_networks.npz, fp32 within 1e-5) and (2) at the C3 size (8192 envs x 20
+e-pucks, cyclamen critic with LSTM memory) against the same module's PyTorch
+path on the same GPU, plus size-independent properties (agent permutation
+equivariance of the baselines)."""
+
+import numpy as np
+import pytest
+import torch
+
+import networks_io as IO
+from SwarmACB_isaac.agents import poca_networks as PN
+
+pytestmark = pytest.mark.gpu
+
+G = IO.load()
+TOL = dict(rtol=1e-5, atol=1e-5)
+
+
+@pytest.fixture
+def fused_calls(monkeypatch):
+    calls = []
+    orig = PN._fused_rsa
+
+    def spy(attn, rows, mode, n):
+        calls.append(mode)
+        return orig(attn, rows, mode, n)
+
+    monkeypatch.setattr(PN, "_fused_rsa", spy)
+    return calls
+
+
+def close(got, key):
+    np.testing.assert_allclose(got.detach().cpu().numpy(), G[key], err_msg=key, **TOL)
+
+
+@pytest.mark.parametrize("prefix", IO.CRITICS)
+def test_fused_critic_matches_reference(gpu_device, fused_calls, prefix):
+    c = IO.critic(G, prefix, gpu_device)
+    s, a = IO.t(G, prefix + "states", gpu_device), IO.t(G, prefix + "actions", gpu_device)
+    with torch.no_grad():
+        close(PN._fused_rsa(c.self_attn, c.obs_entity_enc(s), 0, 20), prefix + "pool_critic")
+        rows = torch.cat([c.obs_entity_enc(s), c.obs_act_entity_enc(torch.cat([s, a], -1))], 1)
+        close(PN._fused_rsa(c.self_attn, rows, 1, 20), prefix + "pool_baselines")
+        close(c.critic_pass(s), prefix + "critic_pass")
+        close(c.joint_action_pass(s, a), prefix + "joint_action_pass")
+        close(c.all_baselines(s, a), prefix + "all_baselines")
+        close(c.baseline(s[:, 3], torch.cat([s[:, :3], s[:, 4:]], 1), torch.cat([a[:, :3], a[:, 4:]], 1)),
+              prefix + "baseline3")
+        if c.lstm is not None:
+            mc = (IO.t(G, prefix + "mem_critic_h", gpu_device), IO.t(G, prefix + "mem_critic_c", gpu_device))
+            mb = (IO.t(G, prefix + "mem_base_h", gpu_device), IO.t(G, prefix + "mem_base_c", gpu_device))
+            v, (vh, vc) = c.critic_pass(s, mc, return_memory=True)
+            close(v, prefix + "critic_pass_mem"), close(vh, prefix + "critic_pass_mem_h")
+            b, (bh, bc) = c.all_baselines(s, a, mb, return_memory=True)
+            close(b, prefix + "all_baselines_mem"), close(bh, prefix + "all_baselines_mem_h")
+            close(bc, prefix + "all_baselines_mem_c")
+    assert 1 in fused_calls and 0 in fused_calls  # both kernel modes ran
+
+
+def test_autograd_uses_pytorch_path(gpu_device, fused_calls):
+    c = IO.critic(G, "cyc_", gpu_device)
+    s, a = IO.t(G, "cyc_states", gpu_device), IO.t(G, "cyc_actions", gpu_device)
+    out = c.all_baselines(s, a)
+    out.sum().backward()
+    assert fused_calls == [] and c.self_attn.fc_out.weight.grad is not None
+    close(out, "cyc_all_baselines")
+
+
+@pytest.mark.parametrize("heads", [4, 2, 1])
+def test_fused_matches_torch_path_at_c3_size(gpu_device, heads):
+    """Foraging cyclamen C3: 8192 envs x 20 agents, one-hot module actions,
+    recurrent critic (memory 128)."""
+    torch.manual_seed(heads)
+    E, N = 8192, 20
+    c = PN.POCACritic(5, 6, N, 128, heads, 1, memory_size=128).to(gpu_device).eval()
+    with torch.no_grad():
+        for p in c.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+        s = torch.randn(E, N, 5, device=gpu_device)
+        a = torch.nn.functional.one_hot(torch.randint(0, 6, (E, N), device=gpu_device), 6).float()
+        mem = (torch.randn(1, E * N, 64, device=gpu_device), torch.randn(1, E * N, 64, device=gpu_device))
+        fused, (fh, fc) = c.all_baselines(s, a, mem, return_memory=True)
+        v_fused = c.critic_pass(s)
+        c.use_fused = False
+        ref, (rh, rc) = c.all_baselines(s, a, mem, return_memory=True)
+        v_ref = c.critic_pass(s)
+    torch.testing.assert_close(fused, ref, **TOL)
+    torch.testing.assert_close(fh, rh, **TOL)
+    torch.testing.assert_close(v_fused, v_ref, **TOL)
+
+
+def test_baselines_are_permutation_equivariant(gpu_device):
+    """Relabelling the agents permutes the baselines (the critic is permutation
+    invariant over the other agents; PN:822-882)."""
+    torch.manual_seed(1)
+    c = IO.critic(G, "ff_", gpu_device)
+    s = torch.randn(512, 20, 5, device=gpu_device)
+    a = torch.randn(512, 20, 2, device=gpu_device)
+    perm = torch.randperm(20, device=gpu_device)
+    with torch.no_grad():
+        b = c.all_baselines(s, a)
+        bp = c.all_baselines(s[:, perm], a[:, perm])
+    torch.testing.assert_close(bp, b[:, perm], **TOL)
+
+
+def test_rejects_unsupported_shapes(gpu_device):
+    from SwarmACB_isaac import _native
+    import ctypes as C
+
+    lib = _native.load()
+    z = torch.zeros(4, device=gpu_device)
+    p = C.c_void_p(z.data_ptr())
+    assert lib.swarm_rsa_pool(0, 1, 21, 4, 128, p, p, p, p, p, None) == -1   # N > 20
+    assert lib.swarm_rsa_pool(0, 1, 20, 8, 128, p, p, p, p, p, None) == -1   # 8 heads
+    assert lib.swarm_rsa_pool(0, 1, 20, 4, 256, p, p, p, p, p, None) == -1   # hidden 256
+    assert lib.swarm_rsa_pool(2, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode

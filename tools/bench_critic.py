@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""Measure the fused critic attention (include/swarmcritic.h) at BASELINE.json
+config C3 (Foraging cyclamen POCA: 8192 envs x 20 e-pucks; critic hidden 128,
+4 heads, 1 layer, LSTM memory 128; one-hot behaviour-module actions).
+
+Run through `python bench.py --critic [...]` (its CPU-baseline leg times the
+same module's PyTorch path on the host). Prints one JSON line per stage:
+  * rsa_pool kernel alone (HIP events on the launch stream), algorithmic flops
+    and the fraction of the fp32 matrix-core peak;
+  * all_baselines + critic_pass as the rollout calls them (no_grad), fused vs
+    the PyTorch path of the same module on the same GPU.
+"""
+
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "swarmacb-isaaclab_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+from SwarmACB_isaac import _native  # noqa: E402
+from SwarmACB_isaac.agents import poca_networks as PN  # noqa: E402
+
+MFMA_F32_PEAK = 157.3  # TFLOP/s, MI355X fp32 MFMA (= fp32 vector peak), MI355X_MICROARCH.md
+
+
+def timed(fn, reps):
+    s = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    a.record(s)
+    for _ in range(reps):
+        fn()
+    b.record(s)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=8192)
+    ap.add_argument("--heads", type=int, default=4)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--cpu-envs", type=int, default=64)
+    args = ap.parse_args()
+    E, N, h, H = args.envs, 20, 128, args.heads
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    crit = PN.POCACritic(5, 6, N, h, H, 1, memory_size=128).to(dev).eval()
+    with torch.no_grad():
+        for p in crit.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+    s = torch.randn(E, N, 5, device=dev)
+    a = torch.nn.functional.one_hot(torch.randint(0, 6, (E, N), device=dev), 6).float()
+    mem_b = (torch.zeros(1, E * N, 64, device=dev), torch.zeros(1, E * N, 64, device=dev))
+    mem_c = (torch.zeros(1, E, 64, device=dev), torch.zeros(1, E, 64, device=dev))
+    cfg = {"workload": "POCA critic (cyclamen C3) all_baselines + critic_pass per decision", "num_envs": E,
+           "num_agents": N, "hidden": h, "heads": H, "layers": 1, "memory_size": 128}
+
+    # ---- the kernel alone
+    with torch.no_grad():
+        at = crit.self_attn
+        rows = torch.cat([crit.obs_entity_enc(s), crit.obs_act_entity_enc(torch.cat([s, a], -1))], 1)
+        x = at.embedding_norm(rows).contiguous()
+        w = torch.cat([at.fc_q.weight, at.fc_k.weight, at.fc_v.weight])
+        bq = torch.cat([at.fc_q.bias, at.fc_k.bias, at.fc_v.bias])
+        qkv = torch.nn.functional.linear(x, w, bq).contiguous()
+        pooled = torch.empty(E * N, h, device=dev)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+
+        def kernel():
+            _native.check(lib.swarm_rsa_pool(1, E, N, H, h, ptr(x), ptr(qkv), ptr(at.fc_out.weight),
+                                              ptr(at.fc_out.bias), ptr(pooled), stream), "swarm_rsa_pool")
+
+        sec = timed(kernel, args.reps)
+    R = 2 * N
+    fc_flops = 2.0 * N * N * h * h            # fc_out over the N sets x N rows
+    other = 2.0 * R * R * h + 2.0 * N ** 3 * h  # pair logits (all heads) + P.V
+    flops = E * (fc_flops + other)
+    print(json.dumps({"stage": "rsa_pool_kernel", "ms": sec * 1e3, "algorithmic_flops": flops,
+                      "roofline": {"bound": "mfma", "achieved": flops / sec / 1e12, "peak": MFMA_F32_PEAK,
+                                   "unit": "TFLOP/s", "frac": flops / sec / 1e12 / MFMA_F32_PEAK,
+                                   "mfma_share_of_flops": fc_flops / (fc_flops + other)},
+                      "config": cfg}), flush=True)
+
+    # ---- what the rollout calls per decision (no_grad), fused vs PyTorch path
+    def rollout_calls():
+        with torch.no_grad():
+            crit.critic_pass(s, mem_c, return_memory=True)
+            crit.all_baselines(s, a, mem_b, return_memory=True)
+
+    fused = timed(rollout_calls, args.reps)
+    crit.use_fused = False
+    torch_gpu = timed(rollout_calls, max(3, args.reps // 4))
+    crit.use_fused = True
+    # CPU baseline: the module's PyTorch path (= the reference math) on the host, sample of envs
+    ce = args.cpu_envs
+    cpu = PN.POCACritic(5, 6, N, h, H, 1, memory_size=128).eval()
+    cpu.load_state_dict({k: v.cpu() for k, v in crit.state_dict().items()})
+    sc, ac = s[:ce].cpu(), a[:ce].cpu()
+    with torch.no_grad():
+        cpu.all_baselines(sc, ac)
+        t0 = time.perf_counter()
+        cpu.critic_pass(sc, (mem_c[0][:, :ce].cpu(), mem_c[1][:, :ce].cpu()), return_memory=True)
+        cpu.all_baselines(sc, ac, (mem_b[0][:, :ce * N].cpu(), mem_b[1][:, :ce * N].cpu()), return_memory=True)
+        cpu_s = (time.perf_counter() - t0) * E / ce
+    print(json.dumps({"stage": "critic_rollout_calls", "ms": fused * 1e3, "torch_path_gpu_ms": torch_gpu * 1e3,
+                      "speedup_vs_torch_gpu": torch_gpu / fused,
+                      "cpu_baseline": {"ms": cpu_s * 1e3, "kind": "port", "cores": torch.get_num_threads(),
+                                       "sample": f"same module, PyTorch path on host CPU, {ce} envs, scaled x{E / ce:g}"},
+                      "config": cfg}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
