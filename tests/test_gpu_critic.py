@@ -62,7 +62,7 @@ def test_fused_critic_matches_reference(gpu_device, fused_calls, prefix):
 
 
 def test_autograd_uses_pytorch_path(gpu_device, fused_calls):
-    c = IO.critic(G, "cyc_", gpu_device)
+    c = IO.critic(G, "cyc_", gpu_device).train()   # MIOpen's LSTM backward needs training mode
     s, a = IO.t(G, "cyc_states", gpu_device), IO.t(G, "cyc_actions", gpu_device)
     out = c.all_baselines(s, a)
     out.sum().backward()
