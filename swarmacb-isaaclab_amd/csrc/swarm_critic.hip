@@ -14,8 +14,8 @@
 //   phase 0  stages x, q, k, v of one env in LDS;
 //   phase 1  computes the attention logits of every entity pair and head
 //            (all sets of the env share them);
-//   phase 2  walks the sets four at a time (one per wave): softmax + P.V on the
-//            VALU, then fc_out for the chunk's 4N rows on the matrix cores
+//   phase 2  walks the sets four at a time (one per wave): softmax on the VALU,
+//            P.V per head and fc_out for the chunk's 4N rows on the matrix cores
 //            (v_mfma_f32_16x16x4_f32, exact fp32 products; W_out is held in
 //            VGPRs as B fragments for the whole persistent kernel), bias +
 //            residual, LayerNorm and the mean over the set, written as pooled.
@@ -26,6 +26,12 @@
 #include "../../include/swarmcritic.h"
 #include "../../include/swarmstep.h"
 #include "swarm_launch.h"
+
+// Timing-only ablation switches (tools/critic_ablate.sh; results are WRONG by
+// design): 1 logits, 2 softmax, 4 P.V, 8 fc_out MFMA, 16 LayerNorm + pooling.
+#ifndef RSA_ABLATE
+#define RSA_ABLATE 0
+#endif
 
 namespace {
 
@@ -38,24 +44,22 @@ constexpr int CROWS = SETS * NMAX;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
 // entity row of member k of set s (swarm_rsa_mode_t)
 __device__ __forceinline__ int member(int mode, int N, int s, int k) {
     if (mode == SWARM_RSA_SINGLE) return k;
     return k == 0 ? s : N + (k - 1 < s ? k - 1 : k);
 }
 
-template <int NH>
-__global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, const float* __restrict__ X,
+// NC: set size as a compile-time constant (the reference's 20 e-pucks), or 0 =
+// runtime n_rt. A compile-time set size lets every per-member loop unroll
+// without predicates, so the LDS reads of a loop are all in flight at once:
+// with one wave per SIMD nothing else hides their latency.
+template <int NH, int NC>
+__global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt, const float* __restrict__ X,
                                                        const float* __restrict__ QKV, const float* __restrict__ Wo,
                                                        const float* __restrict__ bo, float* __restrict__ pooled) {
+    const int N = NC > 0 ? NC : n_rt;
     constexpr int DH = HD / NH;   // head width
-    constexpr int CW = DH / 4;    // output channels per P.V work item
     const int R = mode == SWARM_RSA_SINGLE ? N : 2 * N;
     const int n_sets = mode == SWARM_RSA_SINGLE ? 1 : N;
 
@@ -103,7 +107,7 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, c
         }
         __syncthreads();
         // ---- phase 1: logits of every entity pair and head
-        for (int e = tid; e < NH * R * R; e += 256) {
+        for (int e = tid; e < ((RSA_ABLATE & 1) ? 0 : NH * R * R); e += 256) {
             const int h = e / (R * R);
             const int rem = e - h * R * R;
             const int qr = rem / R, kr = rem - (rem / R) * R;
@@ -128,7 +132,7 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, c
             const bool have = set < n_sets;
             float* P = &PF[wave * NH * NMAX * NMAX];
             // 2a-1: softmax over the set's members for every (row, head)
-            if (have) {
+            if (have && !(RSA_ABLATE & 2)) {
                 for (int p = lane; p < N * NH; p += 64) {
                     const int r = p / NH, h = p - (p / NH) * NH;
                     const float* srow = &S[(h * RMAX + member(mode, N, set, r)) * RMAX];
@@ -144,50 +148,55 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, c
 #pragma unroll
                     for (int k = 0; k < NMAX; ++k)
                         if (k < N) {
-                            l[k] = expf(l[k] - m);
+                            l[k] = __expf(l[k] - m);
                             sum += l[k];
                         }
+                    const float inv = 1.0f / sum;
                     float* prow = &P[(h * NMAX + r) * NMAX];
 #pragma unroll
-                    for (int k = 0; k < NMAX; ++k)
-                        if (k < N) prow[k] = l[k] / sum;
+                    for (int k = 0; k < NMAX; ++k) prow[k] = k < N ? l[k] * inv : 0.0f;
                 }
             }
             __syncthreads();
-            // 2a-2: attention outputs O[row][h*DH + c] = sum_k P[h][row][k] v[member k][h*DH + c]
-            if (have) {
-                for (int it = lane; it < N * NH * 4; it += 64) {
-                    const int r = it / (NH * 4);
-                    const int rem = it - r * (NH * 4);
-                    const int h = rem >> 2, c0 = h * DH + (rem & 3) * CW;
-                    const float* prow = &P[(h * NMAX + r) * NMAX];
-                    float4 o[CW / 4];
+            // 2a-2: attention outputs O[row][h*DH + c] = sum_k P[h][row][k] v[member k][h*DH + c],
+            // per head a (N x N) x (N x DH) product on the matrix cores: rows in two 16-row
+            // tiles (rows >= N discarded), members in 5 k-steps of 4 (zero-padded past N).
+            if (have && !(RSA_ABLATE & 4)) {
+                constexpr int KS = NMAX / 4;
+                const int kq = lane >> 4, cl = lane & 15;
 #pragma unroll
-                    for (int c = 0; c < CW / 4; ++c) o[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int h = 0; h < NH; ++h) {
 #pragma unroll
-                    for (int k = 0; k < NMAX; ++k)
-                        if (k < N) {
-                            const float pk = prow[k];
-                            const float* vrow = &Vs[member(mode, N, set, k) * LDSW + c0];
+                    for (int nt = 0; nt < DH / 16; ++nt) {
+                        const int col = h * DH + nt * 16 + cl;
+                        float bv[KS];
 #pragma unroll
-                            for (int c = 0; c < CW / 4; ++c) {
-                                const float4 v = *reinterpret_cast<const float4*>(vrow + 4 * c);
-                                o[c].x += pk * v.x;
-                                o[c].y += pk * v.y;
-                                o[c].z += pk * v.z;
-                                o[c].w += pk * v.w;
-                            }
+                        for (int ks = 0; ks < KS; ++ks) {
+                            const int k = 4 * ks + kq;
+                            bv[ks] = Vs[member(mode, N, set, k < N ? k : 0) * LDSW + col];
                         }
-                    float* orow = &QKO[(wave * N + r) * LDSW + c0];
+                        const float* p0 = &P[(h * NMAX + cl) * NMAX + kq];
+                        const float* p1 = p0 + 16 * NMAX;
+                        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int c = 0; c < CW / 4; ++c) *reinterpret_cast<float4*>(orow + 4 * c) = o[c];
+                        for (int ks = 0; ks < KS; ++ks) {
+                            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(p0[4 * ks], bv[ks], acc0, 0, 0, 0);
+                            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(p1[4 * ks], bv[ks], acc1, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int r0 = 4 * kq + i, r1 = 16 + 4 * kq + i;
+                            if (r0 < N) QKO[(wave * N + r0) * LDSW + col] = acc0[i];
+                            if (r1 < N) QKO[(wave * N + r1) * LDSW + col] = acc1[i];
+                        }
+                    }
                 }
             }
             __syncthreads();
             // 2b: fc_out on the matrix cores. Rows = the chunk's set rows (16-row tiles),
             // this wave's 32 columns as two 16-column tiles sharing the A operand.
             const int rows = min(SETS, n_sets - s0) * N;
-            const int mtiles = (rows + 15) >> 4;
+            const int mtiles = (RSA_ABLATE & 8) ? 0 : (rows + 15) >> 4;
             for (int mt = 0; mt < mtiles; ++mt) {
                 f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
                 const float* arow = &QKO[(mt * 16 + (lane & 15)) * LDSW + 32 * q];
@@ -218,18 +227,40 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int N, c
                 }
             }
             __syncthreads();
-            // 2c: LayerNorm (no affine, eps 1e-5) of every row of this wave's set, mean over the set
-            if (have) {
-                float p0 = 0.0f, p1 = 0.0f;
-                for (int r = 0; r < N; ++r) {
-                    const float2 f = *reinterpret_cast<const float2*>(&PF[(wave * N + r) * LDSW + 2 * lane]);
-                    const float mean = wave_sum(f.x + f.y) * (1.0f / HD);
-                    const float d0 = f.x - mean, d1 = f.y - mean;
-                    const float var = wave_sum(d0 * d0 + d1 * d1) * (1.0f / HD);
-                    const float rstd = 1.0f / sqrtf(var + 1e-5f);
-                    p0 += d0 * rstd;
-                    p1 += d1 * rstd;
+            // 2c: LayerNorm (no affine, eps 1e-5) of every row of this wave's set, mean over the set.
+            // Row statistics: one lane per row walks its row (no cross-lane reductions);
+            // then each lane pools two columns over the rows. Stats live where O was.
+            float* stats = &QKO[wave * 2 * NMAX];
+            if (have && !(RSA_ABLATE & 16) && lane < N) {
+                const float4* fr = reinterpret_cast<const float4*>(&PF[(wave * N + lane) * LDSW]);
+                float sum = 0.0f;
+#pragma unroll
+                for (int c = 0; c < HD / 4; ++c) {
+                    const float4 v = fr[c];
+                    sum += (v.x + v.y) + (v.z + v.w);
                 }
+                const float mean = sum * (1.0f / HD);
+                float sq = 0.0f;
+#pragma unroll
+                for (int c = 0; c < HD / 4; ++c) {
+                    const float4 v = fr[c];
+                    const float d0 = v.x - mean, d1 = v.y - mean, d2 = v.z - mean, d3 = v.w - mean;
+                    sq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+                }
+                stats[2 * lane] = mean;
+                stats[2 * lane + 1] = 1.0f / sqrtf(sq * (1.0f / HD) + 1e-5f);
+            }
+            __syncthreads();
+            if (have && !(RSA_ABLATE & 16)) {
+                float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+                for (int r = 0; r < NMAX; ++r)
+                    if (r < N) {
+                        const float2 f = *reinterpret_cast<const float2*>(&PF[(wave * N + r) * LDSW + 2 * lane]);
+                        const float mean = stats[2 * r], rstd = stats[2 * r + 1];
+                        p0 += (f.x - mean) * rstd;
+                        p1 += (f.y - mean) * rstd;
+                    }
                 *reinterpret_cast<float2*>(&pooled[((size_t)b * n_sets + set) * HD + 2 * lane]) =
                     make_float2(p0 / (float)N, p1 / (float)N);
             }
@@ -261,12 +292,17 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
     }
     const int grid = B < g_cus ? B : g_cus;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    const bool n20 = N == NMAX;  // the reference swarm: compile-time set size
+#define RSA_LAUNCH(NH)                                                                                   \
+    (n20 ? rsa_pool_kernel<NH, NMAX><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)      \
+         : rsa_pool_kernel<NH, 0><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
     if (heads == 1)
-        rsa_pool_kernel<1><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+        RSA_LAUNCH(1);
     else if (heads == 2)
-        rsa_pool_kernel<2><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+        RSA_LAUNCH(2);
     else
-        rsa_pool_kernel<4><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled);
+        RSA_LAUNCH(4);
+#undef RSA_LAUNCH
     return swarm::record_hip_status();
 }
 

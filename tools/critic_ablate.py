@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Time the critic-kernel ablation variants built by tools/critic_ablate.sh (GPU)."""
+import ctypes as C
+import glob
+import json
+import os
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+E, N, h, H = 8192, 20, 128, 4
+dev = torch.device("cuda:0")
+x = torch.randn(E, 2 * N, h, device=dev)
+qkv = torch.randn(E, 2 * N, 3 * h, device=dev)
+wo = torch.randn(h, h, device=dev) * 0.05
+bo = torch.randn(h, device=dev)
+out = torch.empty(E * N, h, device=dev)
+p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+res = {}
+for path in sorted(glob.glob(os.path.join(ROOT, "build/ablate/libcritic_*.so"))):
+    lib = C.CDLL(path)
+    lib.swarm_rsa_pool.argtypes = [C.c_int32] * 5 + [C.c_void_p] * 6
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    run = lambda: lib.swarm_rsa_pool(1, E, N, H, h, p(x), p(qkv), p(wo), p(bo), p(out), s)  # noqa: E731
+    assert run() == 0
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(10):
+        run()
+    b.record()
+    torch.cuda.synchronize()
+    res[os.path.basename(path)] = a.elapsed_time(b) / 10
+print(json.dumps(res, indent=1))

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build timing-only ablation variants of the critic kernel as standalone .so files
+# (build/ablate/libcritic_<mask>.so); time them with tools/critic_ablate.py on the GPU.
+set -e
+cd "$(dirname "$0")/../swarmacb-isaaclab_amd/csrc"
+OUT=../../build/ablate
+mkdir -p $OUT
+cat > $OUT/stub.cpp <<'EOS'
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+namespace swarm { int32_t record_hip_status() { return hipGetLastError() == hipSuccess ? 0 : -3; } }
+EOS
+for m in ${MASKS:-0 1 2 4 8 16 6}; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -shared -DRSA_ABLATE=$m \
+    -o $OUT/libcritic_$m.so swarm_critic.hip $OUT/stub.cpp &
+done
+wait
+ls $OUT

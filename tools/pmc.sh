@@ -7,7 +7,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-make -C swarmacb-isaaclab_amd/csrc > gpurun_out/pmc/build.log 2>&1 || exit 2
+test -f swarmacb-isaaclab_amd/SwarmACB_isaac/libswarmstep.so || exit 2
 ARGS="--cpu-seconds 0 --steps ${PMC_STEPS:-100} --warmup 10 ${BENCH_ARGS:-}"
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/avail.txt 2>&1 || echo "rocprofv3 -L rc=$?"
 run_pass() {
