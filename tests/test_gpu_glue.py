@@ -181,3 +181,98 @@ def test_collector_matches_substep_loop(gpu_device, steps_before):
     assert ret == glue.returns and length == glue.lengths and group == glue.group
     if steps_before:
         assert len(ret) == E  # every env timed out once inside the rollout
+
+
+def _reference_loop_recurrent(env, actor, critic, buf, obs_dict, R, dp, strength, mem):
+    """poca_trainer.py:461-646 restated for the recurrent discrete (cyclamen) branch,
+    env stepped per substep; mem = dict of the six LSTM memories."""
+    agents = env.possible_agents
+    E, N = env.num_envs, env.num_agents
+    glue = RO.DecisionGlue(E)
+    for _ in range(R):
+        obs = torch.stack([obs_dict[a] for a in agents], dim=1)
+        memory_h = mem["ah"].squeeze(0).view(E, N, -1).clone()
+        memory_c = mem["ac"].squeeze(0).view(E, N, -1).clone()
+        logits, nm = actor.step(obs.reshape(E * N, -1), (mem["ah"], mem["ac"]))
+        mem["ah"], mem["ac"] = nm[0].detach(), nm[1].detach()
+        dist = torch.distributions.Categorical(logits=logits)
+        act = dist.sample()
+        all_actions, all_logp = act.view(E, N, 1), dist.log_prob(act).view(E, N, 1)
+        cs = env.get_critic_state()
+        onehot = torch.nn.functional.one_hot(all_actions.squeeze(-1).long(), 6).float()
+        cmh, cmc = mem["ch"].squeeze(0).clone(), mem["cc"].squeeze(0).clone()
+        bmh = mem["bh"].squeeze(0).view(E, N, -1).clone()
+        bmc = mem["bc"].squeeze(0).view(E, N, -1).clone()
+        tv, ncm = critic.critic_pass(cs, (mem["ch"], mem["cc"]), return_memory=True)
+        bl, nbm = critic.all_baselines(cs, onehot, (mem["bh"], mem["bc"]), return_memory=True)
+        mem["ch"], mem["cc"] = ncm[0].detach(), ncm[1].detach()
+        mem["bh"], mem["bc"] = nbm[0].detach(), nbm[1].detach()
+        action_dict = {a: all_actions[:, i] for i, a in enumerate(agents)}
+        acc = torch.zeros(E, device=env.device)
+        last = torch.zeros(E, device=env.device)
+        for _dp in range(dp):
+            obs_dict, rew, term, trunc, _ = env.step(action_dict)
+            acc += rew[agents[0]]
+            last = torch.max(last, (term[agents[0]] | trunc[agents[0]]).float())
+        tvo = critic.critic_pass(env.completed_terminal_critic_state, (mem["ch"], mem["cc"])).squeeze(-1)
+        row = glue.record(acc.cpu().numpy(), last.cpu().numpy(), env.completed_group_reward.cpu().numpy(),
+                          tvo.cpu().numpy(), dp, strength)
+        d = lambda k: torch.as_tensor(row[k]).to(env.device)  # noqa: E731
+        buf.add(obs, cs, all_actions, all_logp, d("rewards"), d("dones"), d("timeouts"), d("timeout_values"),
+                tv.squeeze(-1), bl, memory_h=memory_h, memory_c=memory_c, critic_memory_h=cmh,
+                critic_memory_c=cmc, baseline_memory_h=bmh, baseline_memory_c=bmc)
+        done = last.bool()
+        if done.any():
+            da = done[:, None].expand(E, N).reshape(-1)
+            for k in ("ah", "ac", "bh", "bc"):
+                mem[k][:, da, :] = 0.0
+            for k in ("ch", "cc"):
+                mem[k][:, done, :] = 0.0
+    buf.compute_returns_and_advantages(critic.critic_pass(env.get_critic_state(), (mem["ch"], mem["cc"])).squeeze(-1))
+    return glue
+
+
+def test_recurrent_collector_matches_substep_loop(gpu_device):
+    """Foraging cyclamen (discrete modules, LSTM actor and critic): a rollout that
+    crosses the 1800-step time-out, so memories of done envs are reset."""
+    from SwarmACB_isaac import ForagingEnvCfg
+    from SwarmACB_isaac.agents.poca_networks import POCACritic, RecurrentDiscreteActor
+
+    E, R, dp = 32, 6, 5
+    torch.manual_seed(0)
+    actor = RecurrentDiscreteActor(4, 6, 128, 1, 128).to(gpu_device)
+    critic = POCACritic(5, 6, 20, 128, 4, 1, memory_size=128).to(gpu_device)
+    envs, bufs = [], []
+    for _ in range(2):
+        cfg = ForagingEnvCfg()
+        cfg.update_variant("cyclamen")
+        cfg.scene.num_envs, cfg.seed = E, 5
+        envs.append(make("SwarmACB-Foraging-v0", cfg, device=gpu_device))
+        bufs.append(POCARolloutBuffer(R, E, 20, obs_dim=4, act_dim=1, memory_size=128, critic_memory_size=128,
+                                      device=gpu_device))
+    obs0 = []
+    for env in envs:
+        obs_dict, _ = env.reset()
+        idle = torch.zeros(E, 20, dtype=torch.int32, device=gpu_device)
+        for _ in range(1785):
+            obs_dict, *_ = env.step(idle)
+        obs0.append(obs_dict)
+    z = lambda n: torch.zeros(1, n, 64, device=gpu_device)  # noqa: E731
+    mem = {"ah": z(E * 20), "ac": z(E * 20), "ch": z(E), "cc": z(E), "bh": z(E * 20), "bc": z(E * 20)}
+    torch.manual_seed(1)
+    with torch.no_grad():
+        glue = _reference_loop_recurrent(envs[0], actor, critic, bufs[0], obs0[0], R, dp, 1.0, mem)
+    torch.manual_seed(1)
+    col = POCARolloutCollector(envs[1], bufs[1], actor, critic, decision_period=dp, discrete=True, num_actions=6,
+                               recurrent=True)
+    col.collect(torch.stack([obs0[1][a] for a in envs[1].possible_agents], dim=1), R)
+    ref, got = bufs[0], bufs[1]
+    for k in ("obs", "critic_states", "actions", "log_probs", "rewards", "dones", "timeouts", "timeout_values",
+              "team_values", "baselines", "returns", "advantages", "memory_h", "memory_c", "critic_memory_h",
+              "critic_memory_c", "baseline_memory_h", "baseline_memory_c"):
+        np.testing.assert_array_equal(getattr(got, k)[:R].cpu().numpy(), getattr(ref, k)[:R].cpu().numpy(),
+                                      err_msg=k)
+    for k, name in (("ah", "actor_memory_h"), ("cc", "critic_memory_c"), ("bh", "baseline_memory_h")):
+        np.testing.assert_array_equal(getattr(col, name).cpu().numpy(), mem[k].cpu().numpy(), err_msg=name)
+    ret, length, group = col.recorder.drain()
+    assert ret == glue.returns and length == glue.lengths and group == glue.group and len(ret) == E
