@@ -248,7 +248,7 @@ def test_recurrent_collector_matches_substep_loop(gpu_device):
         cfg.update_variant("cyclamen")
         cfg.scene.num_envs, cfg.seed = E, 5
         envs.append(make("SwarmACB-Foraging-v0", cfg, device=gpu_device))
-        bufs.append(POCARolloutBuffer(R, E, 20, obs_dim=4, act_dim=1, memory_size=128, critic_memory_size=128,
+        bufs.append(POCARolloutBuffer(R, E, 20, obs_dim=4, act_dim=1, memory_size=64, critic_memory_size=64,
                                       device=gpu_device))
     obs0 = []
     for env in envs:
