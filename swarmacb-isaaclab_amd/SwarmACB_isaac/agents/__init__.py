@@ -4,8 +4,11 @@ option_critic_buffer.py, learned_option_critic_buffer.py), same API, with the
 end-of-rollout scan and the minibatch gathers as HIP kernels."""
 
 from .collector import DecisionRecorder, POCARolloutCollector
+from .config import (FixedOptionCriticConfig, LearnedOptionCriticConfig, POCAConfig, apply_network_settings,
+                     load_config, make_env_cfg)
 from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
 from .option_critic_buffer import FixedOptionRolloutBuffer
 from .poca_buffer import POCARolloutBuffer
 
-__all__ = ["DecisionRecorder", "POCARolloutCollector", "POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer"]
+__all__ = ["DecisionRecorder", "POCARolloutCollector", "POCAConfig", "FixedOptionCriticConfig",
+           "LearnedOptionCriticConfig", "apply_network_settings", "load_config", "make_env_cfg", "POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer"]
