@@ -504,7 +504,11 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
                                                   const float rdx[8], const float rdy[8], float prox[8]) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
-    // wall segments: only those whose line passes within the 0.1 m ray length
+    // wall segments: only those whose line passes within the 0.1 m ray length.
+    // The near segments of this part are collected first and the rays cast only
+    // for them, so the wave loops max(near) times (usually 0-1), not once per
+    // segment of the part. Max is order-free: the readings are unchanged.
+    uint32_t near_mask = 0;
     for (int s = L.p; s < g.nseg; s += ly_parts(LY)) {
         bool near;
         if (s < 12) {
@@ -517,7 +521,11 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float dx = x - (g.iw_ax[k] + u * g.iw_tx[k]), dy = y - (g.iw_ay[k] + u * g.iw_ty[k]);
             near = dx * dx + dy * dy < (g.prox_range + 1e-3f) * (g.prox_range + 1e-3f);
         }
-        if (!near) continue;
+        if (near) near_mask |= 1u << s;
+    }
+    while (near_mask) {
+        const int s = __builtin_ctz(near_mask);
+        near_mask &= near_mask - 1u;
         const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
         const float qx = ax - x, qy = ay - y;
 #pragma unroll
@@ -716,6 +724,32 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             const float dx = q.x - x, dy = q.y - y;
             const float s = dx * dx + dy * dy + 1e-8f;
             if (j != L.i && s < g.rab_range2_hi) cand |= 1ull << j;
+        }
+        if constexpr (ChunkRng<C>::K18) {
+            // One Philox block covers the chunk: draw every candidate's packet-loss
+            // uniform first, then run the term only for the kept neighbours (~15 %),
+            // so the wave loops max(kept) times instead of max(candidates) times.
+            // Same draws, same terms, same increasing-j order as below.
+            unsigned long long kept = 0;
+            if (cand) {
+                const uint4 rb = u_replay ? make_uint4(0, 0, 0, 0)
+                                          : rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), purpose, tick);
+#pragma unroll
+                for (int jj = 0; jj < C; ++jj) {
+                    const int j = L.j0 + jj;
+                    if (j < L.j1 && ((cand >> j) & 1ull)) {
+                        const float uu = u_replay ? u_replay[j] : u01_of7(rb, jj);
+                        if (uu >= g.rab_loss) kept |= 1ull << j;
+                    }
+                }
+            }
+            while (kept) {
+                const int j = __builtin_ctzll(kept);
+                kept &= kept - 1ull;
+                const float2 q = xy[L.ab + j];
+                term(j, q.x - x, q.y - y);
+            }
+            return;
         }
         uint32_t blk = 0xFFFFFFFFu;
         uint4 rb = make_uint4(0, 0, 0, 0);
