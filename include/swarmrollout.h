@@ -107,9 +107,12 @@ int32_t swarm_gather(int32_t mode, const swarm_gather_field_t* fields, int32_t n
  *   for done e, in increasing e: append (episode_reward, episode_steps,
  *     completed_group_reward) to the log at log_count++ (dropped past
  *     log_capacity; log_count still counts), then zero both accumulators
- *   for done e: zero rows [e*rows_per_env, (e+1)*rows_per_env) of every memory slab
+ *   for done e: zero rows [e*rows_per_env, (e+1)*rows_per_env) of every memory slab, and set
+ *     options[e*options_per_env ...] = -1 (the option-critic trainers' current options,
+ *     option_critic_trainer.py:437, learned_option_critic_trainer.py:929)
+ * Up to 12 slabs: POCA uses 6, fixed OC 8, learned OC 10 (LOT:935-944).
  */
-#define SWARM_RECORD_MAX_MEMORIES 8
+#define SWARM_RECORD_MAX_MEMORIES 12
 
 typedef struct {
     float* data;                  /* [E * rows_per_env * width] */
@@ -131,6 +134,9 @@ typedef struct {
     int32_t log_capacity;
     int32_t n_memories;
     swarm_memory_slab_t memories[SWARM_RECORD_MAX_MEMORIES];
+    int64_t* options;             /* [E * options_per_env] current options (nullable) */
+    int32_t options_per_env;
+    int32_t reserved;
 } swarm_decision_record_t;
 
 int32_t swarm_decision_record(int32_t E, int32_t decision_period, double reward_strength,

@@ -70,7 +70,7 @@ class GatherField(C.Structure):
 CRITIC_EXPORTS = ["swarm_rsa_pool"]
 RSA_SINGLE, RSA_BASELINES = 0, 1
 
-RECORD_MAX_MEMORIES = 8
+RECORD_MAX_MEMORIES = 12
 
 
 class MemorySlab(C.Structure):
@@ -81,7 +81,8 @@ class DecisionRecord(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("rewards", "dones", "timeouts", "timeout_values", "episode_reward",
                                           "episode_steps", "log_returns", "log_lengths", "log_group_rewards",
                                           "log_count")] + [
-        ("log_capacity", C.c_int32), ("n_memories", C.c_int32), ("memories", MemorySlab * RECORD_MAX_MEMORIES)]
+        ("log_capacity", C.c_int32), ("n_memories", C.c_int32), ("memories", MemorySlab * RECORD_MAX_MEMORIES),
+        ("options", C.c_void_p), ("options_per_env", C.c_int32), ("reserved", C.c_int32)]
 
 
 _lib = None

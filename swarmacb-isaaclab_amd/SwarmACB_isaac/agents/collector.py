@@ -46,10 +46,11 @@ class DecisionRecorder:
         self.capacity = cap
 
     def record(self, row: dict, reward_sum, truncated, completed_group_reward, decision_period: int,
-               reward_strength: float, timeout_value_raw=None, memories=()):
+               reward_strength: float, timeout_value_raw=None, memories=(), options=None):
         """row: {"rewards", "dones", "timeouts"[, "timeout_values"]} -> (E,) float32 views of
         the buffer row being written. memories: [(tensor, rows_per_env)], rows of done envs
-        are zeroed."""
+        are zeroed. options: (E, N) int64 current options of the option-critic trainers,
+        set to -1 for done envs (option_critic_trainer.py:437)."""
         E = self.num_envs
         rec = _native.DecisionRecord()
         rec.rewards, rec.dones, rec.timeouts = (row["rewards"].data_ptr(), row["dones"].data_ptr(),
@@ -69,6 +70,11 @@ class DecisionRecorder:
             if width * E * rows != m.numel():
                 raise ValueError("memory slab is not (E*rows, width)")
             rec.memories[i] = _native.MemorySlab(m.data_ptr(), rows, width)
+        if options is not None:
+            _dev_check(options)
+            if options.dtype != torch.int64 or options.numel() % E:
+                raise ValueError("options must be an int64 (E, ...) tensor")
+            rec.options, rec.options_per_env = options.data_ptr(), options.numel() // E
         tensors = [reward_sum, truncated, completed_group_reward, timeout_value_raw] + list(row.values())
         _dev_check(*tensors)
         if truncated.dtype not in (torch.uint8, torch.bool):

@@ -345,6 +345,8 @@ __global__ void __launch_bounds__(256) memory_reset_kernel(RecordArgs a, const u
         float* p = s.data + (int64_t)e * n;
         for (int64_t i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0f;
     }
+    if (r.options)
+        for (int i = threadIdx.x; i < r.options_per_env; i += blockDim.x) r.options[(int64_t)e * r.options_per_env + i] = -1;
 }
 
 }  // namespace
@@ -365,12 +367,13 @@ int32_t swarm_decision_record(int32_t E, int32_t decision_period, double reward_
     for (int m = 0; m < rec->n_memories; ++m)
         if (!rec->memories[m].data || rec->memories[m].rows_per_env <= 0 || rec->memories[m].width <= 0)
             return SWARM_ERR_ARG;
+    if (rec->options && rec->options_per_env <= 0) return SWARM_ERR_ARG;
     hipStream_t s = static_cast<hipStream_t>(stream);
     RecordArgs a{*rec};
     // torch multiplies an fp32 tensor by a Python scalar rounded to fp32
     record_kernel<<<1, 1024, 0, s>>>(a, E, (float)decision_period, (float)reward_strength, reward_sum, truncated,
                                      timeout_value_raw, completed_group_reward);
-    if (rec->n_memories > 0) memory_reset_kernel<<<E, 256, 0, s>>>(a, truncated);
+    if (rec->n_memories > 0 || rec->options) memory_reset_kernel<<<E, 256, 0, s>>>(a, truncated);
     return swarm::record_hip_status();
 }
 

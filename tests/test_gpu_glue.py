@@ -276,3 +276,23 @@ def test_recurrent_collector_matches_substep_loop(gpu_device):
         np.testing.assert_array_equal(getattr(col, name).cpu().numpy(), mem[k].cpu().numpy(), err_msg=name)
     ret, length, group = col.recorder.drain()
     assert ret == glue.returns and length == glue.lengths and group == glue.group and len(ret) == E
+
+
+def test_record_learned_option_critic_slabs(gpu_device):
+    """The learned-OC bookkeeping (learned_option_critic_trainer.py:914-944): ten LSTM
+    memory slabs (per agent and per env) and current_options[done] = -1."""
+    E, N, H = 2048, 20, 64
+    rec = DecisionRecorder(E, gpu_device)
+    rows = [N, N, 1, 1, N, N, 1, 1, N, N]
+    mems = [(torch.randn(1, E * r, H, device=gpu_device), r) for r in rows]
+    options = torch.randint(0, 6, (E, N), device=gpu_device)
+    before = [m.clone() for m, _ in mems]
+    opt_before = options.clone()
+    done = torch.rand(E, device=gpu_device) < 0.1
+    ones = torch.ones(E, device=gpu_device)
+    rec.record(_row(E, gpu_device), ones, done.to(torch.uint8), ones, 5, 1.0, timeout_value_raw=ones,
+               memories=mems, options=options)
+    for (m, r), b in zip(mems, before):
+        d = done.repeat_interleave(r)
+        assert (m[0, d] == 0).all() and torch.equal(m[0, ~d], b[0, ~d])
+    assert (options[done] == -1).all() and torch.equal(options[~done], opt_before[~done])
