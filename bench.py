@@ -57,6 +57,8 @@ def parse():
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
                     help="instead of the step: the fused critic attention at C3 (tools/bench_critic.py)")
+    ap.add_argument("--collect", action="store_true",
+                    help="instead of the step: the whole C3 rollout decision loop (tools/bench_collect.py)")
     args, rest = ap.parse_known_args()
     args.rest = rest
     return args
@@ -108,10 +110,14 @@ def load_pmc(envs: int, sub: int) -> dict:
 
 def main():
     args = parse()
-    if args.rollout or args.critic:
+    if args.rollout or args.critic or args.collect:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         sys.argv = [sys.argv[0]] + args.rest
-        if args.rollout:
+        if args.collect:
+            import bench_collect
+
+            bench_collect.main()
+        elif args.rollout:
             import bench_rollout
 
             bench_rollout.main()

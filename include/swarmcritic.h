@@ -42,6 +42,12 @@ typedef enum {
 int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,
                        const float* qkv, const float* w_out, const float* b_out, float* pooled, void* stream);
 
+/* out[r][c] = (in[r][c] - mean_r) / sqrt(var_r + 1e-5) over the hidden = 128 features of each of the
+ * `rows` rows (biased variance): the entity-embedding LayerNorm (no affine) that produces x above,
+ * ResidualSelfAttention.embedding_norm (agents/poca_networks.py:446-491, nn.LayerNorm without
+ * elementwise affine). in/out: [rows][128] f32, 16-byte aligned; in == out allowed. */
+int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

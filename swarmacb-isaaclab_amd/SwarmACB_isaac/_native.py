@@ -67,7 +67,7 @@ class GatherField(C.Structure):
 
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
-CRITIC_EXPORTS = ["swarm_rsa_pool"]
+CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm"]
 RSA_SINGLE, RSA_BASELINES = 0, 1
 
 RECORD_MAX_MEMORIES = 12
@@ -134,6 +134,8 @@ def load() -> C.CDLL:
     lib.swarm_decision_record.argtypes = [i32, i32, C.c_double, vp, vp, vp, vp, C.POINTER(DecisionRecord), vp]
     lib.swarm_rsa_pool.restype = i32
     lib.swarm_rsa_pool.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
+    lib.swarm_rsa_embedding_norm.restype = i32
+    lib.swarm_rsa_embedding_norm.argtypes = [C.c_int64, i32, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

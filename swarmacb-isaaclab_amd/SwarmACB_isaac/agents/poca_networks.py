@@ -231,18 +231,22 @@ def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode: int, n: in
     """Attention pooling of the entity sets of every env through swarm_rsa_pool.
     rows: (B, R, h) embedded entities (R = n, or 2n for the baseline sets)."""
     B = rows.shape[0]
-    x = attn.embedding_norm(rows).contiguous()
+    rows = rows.contiguous()
+    x = torch.empty_like(rows)
+    lib = _native.load()
+    stream = C.c_void_p(torch.cuda.current_stream(rows.device).cuda_stream)
+    _native.check(lib.swarm_rsa_embedding_norm(rows.numel() // attn.embed_dim, attn.embed_dim,
+                                               C.c_void_p(rows.data_ptr()), C.c_void_p(x.data_ptr()), stream),
+                  "swarm_rsa_embedding_norm")
     w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
     b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
     qkv = torch.nn.functional.linear(x, w, b).contiguous()
     n_sets = n if mode == _native.RSA_BASELINES else 1
     pooled = torch.empty(B * n_sets, attn.embed_dim, dtype=torch.float32, device=rows.device)
     wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
-    lib = _native.load()
     rc = lib.swarm_rsa_pool(mode, B, n, attn.num_heads, attn.embed_dim, C.c_void_p(x.data_ptr()),
                             C.c_void_p(qkv.data_ptr()), C.c_void_p(wo.data_ptr()), C.c_void_p(bo.data_ptr()),
-                            C.c_void_p(pooled.data_ptr()),
-                            C.c_void_p(torch.cuda.current_stream(rows.device).cuda_stream))
+                            C.c_void_p(pooled.data_ptr()), stream)
     _native.check(rc, "swarm_rsa_pool")
     return pooled
 

@@ -11,15 +11,16 @@
 // Here the per-entity work is done once per env instead of once per set: the
 // host projects the 2N distinct entity rows (x = LN(embedding), qkv = x W^T,
 // one library GEMM), and this kernel
-//   phase 0  stages x, q, k, v of one env in LDS;
+//   phase 0  stages x, q, k, v of one env in LDS (two envs for the single-set
+//            mode, whose sets are one per env);
 //   phase 1  computes the attention logits of every entity pair and head
 //            (all sets of the env share them);
-//   phase 2  walks the sets four at a time (one per wave): softmax on the VALU,
+//   phase 2  walks the sets four at a time (two waves per set): softmax on the VALU,
 //            P.V per head and fc_out for the chunk's 4N rows on the matrix cores
 //            (v_mfma_f32_16x16x4_f32, exact fp32 products; W_out is held in
 //            VGPRs as B fragments for the whole persistent kernel), bias +
 //            residual, LayerNorm and the mean over the set, written as pooled.
-// One persistent workgroup per CU (4 waves, ~149 KiB of LDS) walks the envs.
+// One persistent workgroup per CU (8 waves, two per SIMD, ~149 KiB of LDS) walks the envs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,34 +39,45 @@ namespace {
 constexpr int HD = 128;           // embedding width (critic hidden_units of the cyclamen / tulip / OC configs)
 constexpr int NMAX = 20;          // entities per set
 constexpr int RMAX = 2 * NMAX;    // entity rows per env
-constexpr int SETS = 4;           // sets per chunk: one per wave
+constexpr int SETS = 4;           // sets per chunk
+constexpr int NT = 512;           // 8 waves: two per set of the chunk, two per SIMD
 constexpr int LDSW = HD + 4;      // padded LDS row stride
 constexpr int CROWS = SETS * NMAX;
+// Logit and probability strides chosen so that the softmax lanes (row r, head h
+// = lane / NH, lane % NH) and the P.V fragment reads hit distinct LDS banks
+// (the unpadded 40 / 1600 strides put 8 lanes on one bank).
+constexpr int SW = 44, SHS = RMAX * SW + 1;      // S[h * SHS + q * SW + k]
+constexpr int PHS = NMAX * NMAX + 1;             // P[h * PHS + r * NMAX + k]
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// entity row of member k of set s (swarm_rsa_mode_t)
+// Envs staged per iteration: SINGLE sets are one per env, so two envs share an
+// iteration (2N <= RMAX rows); BASELINES envs carry N sets each.
+constexpr int SINGLE_ENVS = RMAX / NMAX;
+
+// entity row of member k of set s (swarm_rsa_mode_t); in SINGLE mode set s is
+// the s-th env staged in this iteration
 __device__ __forceinline__ int member(int mode, int N, int s, int k) {
-    if (mode == SWARM_RSA_SINGLE) return k;
+    if (mode == SWARM_RSA_SINGLE) return s * N + k;
     return k == 0 ? s : N + (k - 1 < s ? k - 1 : k);
 }
 
 // NC: set size as a compile-time constant (the reference's 20 e-pucks), or 0 =
 // runtime n_rt. A compile-time set size lets every per-member loop unroll
 // without predicates, so the LDS reads of a loop are all in flight at once:
-// with one wave per SIMD nothing else hides their latency.
+// with two waves per SIMD little else hides their latency.
 template <int NH, int NC>
-__global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt, const float* __restrict__ X,
+__global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt, const float* __restrict__ X,
                                                        const float* __restrict__ QKV, const float* __restrict__ Wo,
                                                        const float* __restrict__ bo, float* __restrict__ pooled) {
     const int N = NC > 0 ? NC : n_rt;
     constexpr int DH = HD / NH;   // head width
-    const int R = mode == SWARM_RSA_SINGLE ? N : 2 * N;
-    const int n_sets = mode == SWARM_RSA_SINGLE ? 1 : N;
+    const bool single = mode == SWARM_RSA_SINGLE;
+    const int iters = single ? (B + SINGLE_ENVS - 1) / SINGLE_ENVS : B;
 
     __shared__ float Xs[RMAX * LDSW];
     __shared__ float Vs[RMAX * LDSW];
-    __shared__ float S[NH * RMAX * RMAX];
+    __shared__ float S[NH * SHS];
     __shared__ float QKO[CROWS * LDSW];  // q | k rows (phases 0-1), then the chunk's attention outputs
     __shared__ float PF[CROWS * LDSW];   // softmax probabilities (2a), then the chunk's fc_out rows (2b-2c)
     float* Qs = QKO;
@@ -73,7 +85,8 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
+    const int wave = (tid >> 6) & (SETS - 1);   // set slot of the chunk / 32-column slice of fc_out
+    const int half = tid >> 8;                  // which of the two waves sharing that slot
     const int q = lane >> 4;      // MFMA k-group of this lane
 
     // W_out^T as MFMA B fragments for this wave's 32 output columns, resident for
@@ -92,25 +105,33 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
     }
     const float sqrt_d = 11.313708498984761f;  // torch divides the logits by math.sqrt(h)
 
-    for (int b = blockIdx.x; b < B; b += gridDim.x) {
-        // ---- phase 0: x, q, k, v rows of this env
-        const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)b * R * HD);
-        const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)b * R * 3 * HD);
-        for (int i = tid; i < R * (HD / 4); i += 256) {
+    for (int it = blockIdx.x; it < iters; it += gridDim.x) {
+        // envs of this iteration (rows of consecutive envs are contiguous), their
+        // entity rows and sets, and the first output row
+        const int e0 = single ? it * SINGLE_ENVS : it;
+        const int n_sets = single ? min(SINGLE_ENVS, B - e0) : N;
+        const int R = single ? n_sets * N : 2 * N;   // = the rows of a set group
+        const int groups = single ? n_sets : 1;      // blocks of rows that attend to each other
+        const int G = R / groups;
+        const size_t out0 = single ? (size_t)e0 : (size_t)e0 * N;
+        // ---- phase 0: x, q, k, v rows of this iteration
+        const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)e0 * (single ? N : 2 * N) * HD);
+        const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)e0 * (single ? N : 2 * N) * 3 * HD);
+        for (int i = tid; i < R * (HD / 4); i += NT) {
             const int r = i / (HD / 4), c = 4 * (i % (HD / 4));
             *reinterpret_cast<float4*>(&Xs[r * LDSW + c]) = x4[i];
         }
-        for (int i = tid; i < R * (3 * HD / 4); i += 256) {
+        for (int i = tid; i < R * (3 * HD / 4); i += NT) {
             const int r = i / (3 * HD / 4), c = 4 * (i % (3 * HD / 4));
             float* dst = c < HD ? &Qs[r * LDSW + c] : c < 2 * HD ? &Ks[r * LDSW + c - HD] : &Vs[r * LDSW + c - 2 * HD];
             *reinterpret_cast<float4*>(dst) = q4[i];
         }
         __syncthreads();
-        // ---- phase 1: logits of every entity pair and head
-        for (int e = tid; e < ((RSA_ABLATE & 1) ? 0 : NH * R * R); e += 256) {
-            const int h = e / (R * R);
-            const int rem = e - h * R * R;
-            const int qr = rem / R, kr = rem - (rem / R) * R;
+        // ---- phase 1: logits of every entity pair and head (within a row group)
+        for (int e = tid; e < ((RSA_ABLATE & 1) ? 0 : NH * R * G); e += NT) {
+            const int h = e / (R * G);
+            const int rem = e - h * R * G;
+            const int qr = rem / G, kr = (qr / G) * G + (rem - qr * G);
             const float* qp = &Qs[qr * LDSW + h * DH];
             const float* kp = &Ks[kr * LDSW + h * DH];
             float acc = 0.0f;
@@ -123,19 +144,19 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
                 acc += u.z * v.z;
                 acc += u.w * v.w;
             }
-            S[(h * RMAX + qr) * RMAX + kr] = acc / sqrt_d;
+            S[h * SHS + qr * SW + kr] = acc / sqrt_d;
         }
         __syncthreads();
-        // ---- phase 2: sets in chunks of SETS (wave w owns set s0 + w)
+        // ---- phase 2: sets in chunks of SETS (waves w and w + 4 own set s0 + w)
         for (int s0 = 0; s0 < n_sets; s0 += SETS) {
             const int set = s0 + wave;
             const bool have = set < n_sets;
-            float* P = &PF[wave * NH * NMAX * NMAX];
+            float* P = &PF[wave * NH * PHS];
             // 2a-1: softmax over the set's members for every (row, head)
             if (have && !(RSA_ABLATE & 2)) {
-                for (int p = lane; p < N * NH; p += 64) {
+                for (int p = lane + 64 * half; p < N * NH; p += 128) {
                     const int r = p / NH, h = p - (p / NH) * NH;
-                    const float* srow = &S[(h * RMAX + member(mode, N, set, r)) * RMAX];
+                    const float* srow = &S[h * SHS + member(mode, N, set, r) * SW];
                     float l[NMAX];
                     float m = -INFINITY;
 #pragma unroll
@@ -152,7 +173,7 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
                             sum += l[k];
                         }
                     const float inv = 1.0f / sum;
-                    float* prow = &P[(h * NMAX + r) * NMAX];
+                    float* prow = &P[h * PHS + r * NMAX];
 #pragma unroll
                     for (int k = 0; k < NMAX; ++k) prow[k] = k < N ? l[k] * inv : 0.0f;
                 }
@@ -164,18 +185,19 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
             if (have && !(RSA_ABLATE & 4)) {
                 constexpr int KS = NMAX / 4;
                 const int kq = lane >> 4, cl = lane & 15;
+                // the 8 (head, 16-column) tiles: four per wave of the pair
 #pragma unroll
-                for (int h = 0; h < NH; ++h) {
-#pragma unroll
-                    for (int nt = 0; nt < DH / 16; ++nt) {
-                        const int col = h * DH + nt * 16 + cl;
+                for (int t = 0; t < 4; ++t) {
+                    {
+                        const int tile = 4 * half + t, h = tile / (DH / 16);
+                        const int col = tile * 16 + cl;
                         float bv[KS];
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int k = 4 * ks + kq;
                             bv[ks] = Vs[member(mode, N, set, k < N ? k : 0) * LDSW + col];
                         }
-                        const float* p0 = &P[(h * NMAX + cl) * NMAX + kq];
+                        const float* p0 = &P[h * PHS + cl * NMAX + kq];
                         const float* p1 = p0 + 16 * NMAX;
                         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -194,10 +216,11 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
             }
             __syncthreads();
             // 2b: fc_out on the matrix cores. Rows = the chunk's set rows (16-row tiles),
-            // this wave's 32 columns as two 16-column tiles sharing the A operand.
+            // this wave's 32 columns as two 16-column tiles sharing the A operand; the two
+            // waves of a slot take alternate row tiles.
             const int rows = min(SETS, n_sets - s0) * N;
             const int mtiles = (RSA_ABLATE & 8) ? 0 : (rows + 15) >> 4;
-            for (int mt = 0; mt < mtiles; ++mt) {
+            for (int mt = half; mt < mtiles; mt += 2) {
                 f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
                 const float* arow = &QKO[(mt * 16 + (lane & 15)) * LDSW + 32 * q];
 #pragma unroll
@@ -231,7 +254,7 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
             // Row statistics: one lane per row walks its row (no cross-lane reductions);
             // then each lane pools two columns over the rows. Stats live where O was.
             float* stats = &QKO[wave * 2 * NMAX];
-            if (have && !(RSA_ABLATE & 16) && lane < N) {
+            if (have && !(RSA_ABLATE & 16) && half == 0 && lane < N) {
                 const float4* fr = reinterpret_cast<const float4*>(&PF[(wave * N + lane) * LDSW]);
                 float sum = 0.0f;
 #pragma unroll
@@ -252,21 +275,36 @@ __global__ void __launch_bounds__(256) rsa_pool_kernel(int mode, int B, int n_rt
             }
             __syncthreads();
             if (have && !(RSA_ABLATE & 16)) {
-                float p0 = 0.0f, p1 = 0.0f;
+                const int col = 64 * half + lane;
+                float p0 = 0.0f;
 #pragma unroll
                 for (int r = 0; r < NMAX; ++r)
-                    if (r < N) {
-                        const float2 f = *reinterpret_cast<const float2*>(&PF[(wave * N + r) * LDSW + 2 * lane]);
-                        const float mean = stats[2 * r], rstd = stats[2 * r + 1];
-                        p0 += (f.x - mean) * rstd;
-                        p1 += (f.y - mean) * rstd;
-                    }
-                *reinterpret_cast<float2*>(&pooled[((size_t)b * n_sets + set) * HD + 2 * lane]) =
-                    make_float2(p0 / (float)N, p1 / (float)N);
+                    if (r < N) p0 += (PF[(wave * N + r) * LDSW + col] - stats[2 * r]) * stats[2 * r + 1];
+                pooled[(out0 + set) * HD + col] = p0 / (float)N;
             }
             __syncthreads();
         }
     }
+}
+
+// LayerNorm without affine (eps 1e-5) of 128-wide rows: 32 lanes x float4 per
+// row, 8 rows per 256-thread block; one HBM read and one write per element.
+__global__ void __launch_bounds__(256) embedding_norm_kernel(int64_t rows, const float4* __restrict__ in,
+                                                             float4* __restrict__ out) {
+    const int64_t row = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
+    if (row >= rows) return;
+    const int64_t i = row * (HD / 4) + (threadIdx.x & 31);
+    const float4 v = in[i];
+    float s = (v.x + v.y) + (v.z + v.w);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
+    const float mean = s * (1.0f / HD);
+    const float4 d = make_float4(v.x - mean, v.y - mean, v.z - mean, v.w - mean);
+    float q = (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 32);
+    const float rstd = 1.0f / sqrtf(q * (1.0f / HD) + 1e-5f);
+    out[i] = make_float4(d.x * rstd, d.y * rstd, d.z * rstd, d.w * rstd);
 }
 
 int g_cus = 0;
@@ -290,12 +328,13 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
             cus = 256;
         g_cus = cus;
     }
-    const int grid = B < g_cus ? B : g_cus;
+    const int iters = mode == SWARM_RSA_SINGLE ? (B + SINGLE_ENVS - 1) / SINGLE_ENVS : B;
+    const int grid = iters < g_cus ? iters : g_cus;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool n20 = N == NMAX;  // the reference swarm: compile-time set size
 #define RSA_LAUNCH(NH)                                                                                   \
-    (n20 ? rsa_pool_kernel<NH, NMAX><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)      \
-         : rsa_pool_kernel<NH, 0><<<grid, 256, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
+    (n20 ? rsa_pool_kernel<NH, NMAX><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)       \
+         : rsa_pool_kernel<NH, 0><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
     if (heads == 1)
         RSA_LAUNCH(1);
     else if (heads == 2)
@@ -303,6 +342,17 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
     else
         RSA_LAUNCH(4);
 #undef RSA_LAUNCH
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, float* out, void* stream) {
+    if (hidden != HD || rows < 0) return SWARM_ERR_ARG;
+    if (rows == 0) return SWARM_OK;
+    if (!in || !out || ((((uintptr_t)in) | ((uintptr_t)out)) & 15)) return SWARM_ERR_ARG;
+    const int64_t blocks = (rows + 7) / 8;
+    if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
+    embedding_norm_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
+        rows, reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out));
     return swarm::record_hip_status();
 }
 

@@ -118,3 +118,37 @@ def test_rejects_unsupported_shapes(gpu_device):
     assert lib.swarm_rsa_pool(0, 1, 20, 8, 128, p, p, p, p, p, None) == -1   # 8 heads
     assert lib.swarm_rsa_pool(0, 1, 20, 4, 256, p, p, p, p, p, None) == -1   # hidden 256
     assert lib.swarm_rsa_pool(2, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode
+
+
+@pytest.mark.parametrize("B,N,heads", [(1, 20, 4), (7, 20, 2), (5, 13, 4), (9, 3, 1), (2, 1, 4)])
+def test_single_sets_odd_env_counts(gpu_device, B, N, heads):
+    """SINGLE mode stages two envs per iteration: odd env counts (a last iteration
+    with one env), runtime set sizes and N = 1 against the module's PyTorch path."""
+    torch.manual_seed(B * 100 + N)
+    c = PN.POCACritic(5, 2, N, 128, heads, 1).to(gpu_device).eval()
+    s = torch.randn(B, N, 5, device=gpu_device)
+    a = torch.randn(B, N, 2, device=gpu_device)
+    with torch.no_grad():
+        v, q = c.critic_pass(s), c.joint_action_pass(s, a)
+        bl = c.all_baselines(s, a) if N > 1 else None
+        c.use_fused = False
+        torch.testing.assert_close(v, c.critic_pass(s), **TOL)
+        torch.testing.assert_close(q, c.joint_action_pass(s, a), **TOL)
+        if bl is not None:
+            torch.testing.assert_close(bl, c.all_baselines(s, a), **TOL)
+
+
+@pytest.mark.parametrize("rows", [1, 7, 8, 163841])
+def test_embedding_norm_matches_layer_norm(gpu_device, rows):
+    from SwarmACB_isaac import _native
+    import ctypes as C
+
+    torch.manual_seed(rows)
+    x = torch.randn(rows, 128, device=gpu_device) * 3.0 + 0.5
+    out = torch.full_like(x, float("nan"))
+    lib = _native.load()
+    rc = lib.swarm_rsa_embedding_norm(rows, 128, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out, torch.nn.functional.layer_norm(x, (128,)), **TOL)
+    assert lib.swarm_rsa_embedding_norm(rows, 64, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), None) == -1

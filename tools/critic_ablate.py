@@ -9,9 +9,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 E, N, h, H = 8192, 20, 128, 4
+MODE = int(os.environ.get("RSA_MODE", "1"))   # 1 all_baselines sets, 0 one set per env (critic_pass)
+R = 2 * N if MODE == 1 else N
 dev = torch.device("cuda:0")
-x = torch.randn(E, 2 * N, h, device=dev)
-qkv = torch.randn(E, 2 * N, 3 * h, device=dev)
+x = torch.randn(E, R, h, device=dev)
+qkv = torch.randn(E, R, 3 * h, device=dev)
 wo = torch.randn(h, h, device=dev) * 0.05
 bo = torch.randn(h, device=dev)
 out = torch.empty(E * N, h, device=dev)
@@ -21,7 +23,7 @@ for path in sorted(glob.glob(os.path.join(ROOT, "build/ablate/libcritic_*.so")))
     lib = C.CDLL(path)
     lib.swarm_rsa_pool.argtypes = [C.c_int32] * 5 + [C.c_void_p] * 6
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    run = lambda: lib.swarm_rsa_pool(1, E, N, H, h, p(x), p(qkv), p(wo), p(bo), p(out), s)  # noqa: E731
+    run = lambda: lib.swarm_rsa_pool(MODE, E, N, H, h, p(x), p(qkv), p(wo), p(bo), p(out), s)  # noqa: E731
     assert run() == 0
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
