@@ -48,6 +48,15 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
  * elementwise affine). in/out: [rows][128] f32, 16-byte aligned; in == out allowed. */
 int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, float* out, void* stream);
 
+/* One time step of a single-layer LSTM (the ML-Agents memory of the recurrent actor and critic:
+ * RecurrentDiscreteActor.forward_sequence poca_networks.py:320-414 and POCACritic's memory LSTM
+ * :596-625, torch.nn.LSTM with sequence length 1) from its gate pre-activations
+ * gates[r] = x[r] W_ih^T + b_ih + h[r] W_hh^T + b_hh, [n][4 * units] in torch's i | f | g | o order:
+ *   c_out = sigmoid(f) * c_prev + sigmoid(i) * tanh(g),  h_out = sigmoid(o) * tanh(c_out).
+ * c_prev, h_out, c_out: [n][units] f32; c_out may alias c_prev. */
+int32_t swarm_lstm_cell(int64_t n, int32_t units, const float* gates, const float* c_prev, float* h_out,
+                        float* c_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,7 +67,7 @@ class GatherField(C.Structure):
 
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
-CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm"]
+CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
 RSA_SINGLE, RSA_BASELINES = 0, 1
 
 RECORD_MAX_MEMORIES = 12
@@ -136,6 +136,8 @@ def load() -> C.CDLL:
     lib.swarm_rsa_pool.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     lib.swarm_rsa_embedding_norm.restype = i32
     lib.swarm_rsa_embedding_norm.argtypes = [C.c_int64, i32, vp, vp, vp]
+    lib.swarm_lstm_cell.restype = i32
+    lib.swarm_lstm_cell.argtypes = [C.c_int64, i32, vp, vp, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -68,6 +68,34 @@ def _mlagents_lstm(input_size: int, memory_size: int, forget_bias: float = 1.0) 
     return lstm, units
 
 
+FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of the reference path)
+
+
+def _lstm(lstm: nn.LSTM, seq: torch.Tensor, state):
+    """lstm(seq, state) for a batch-first single-layer nn.LSTM. Rollout-time calls
+    (one step, no autograd, on the GPU) take the fused path: the gate
+    pre-activations as two library GEMMs, then swarm_lstm_cell (include/swarmcritic.h)
+    for the cell update; everything else runs torch's LSTM."""
+    n, T, _ = seq.shape
+    if not (FUSED_LSTM and T == 1 and seq.is_cuda and not torch.is_grad_enabled() and lstm.num_layers == 1
+            and not lstm.bidirectional and lstm.batch_first and lstm.proj_size == 0 and lstm.bias):
+        return lstm(seq, state)
+    units = lstm.hidden_size
+    h0, c0 = state
+    h0 = h0.reshape(n, units)
+    c0 = c0.reshape(n, units).contiguous()
+    gates = torch.nn.functional.linear(seq.reshape(n, -1), lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
+    gates.addmm_(h0, lstm.weight_hh_l0.t())
+    h1 = torch.empty(1, n, units, dtype=seq.dtype, device=seq.device)
+    c1 = torch.empty_like(h1)
+    lib = _native.load()
+    rc = lib.swarm_lstm_cell(n, units, C.c_void_p(gates.data_ptr()), C.c_void_p(c0.data_ptr()),
+                             C.c_void_p(h1.data_ptr()), C.c_void_p(c1.data_ptr()),
+                             C.c_void_p(torch.cuda.current_stream(seq.device).cuda_stream))
+    _native.check(rc, "swarm_lstm_cell")
+    return h1.view(n, 1, units), (h1, c1)
+
+
 def checkpoint_memory_size(checkpoint: dict, default: int = 128) -> int:
     """Total ML-Agents memory size of a checkpoint (poca_networks.py:116-127):
     checkpoints older than the parity revision stored the LSTM unit count."""
@@ -168,7 +196,7 @@ class RecurrentDiscreteActor(nn.Module):
     def forward_sequence(self, obs_seq: torch.Tensor, state=None):
         B, T = obs_seq.shape[:2]
         enc = self.net(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
-        out, nxt = self.lstm(enc, state if state is not None else self.initial_state(B, obs_seq.device))
+        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device))
         return self.logits_head(out), nxt
 
     def step(self, obs: torch.Tensor, state=None):
@@ -305,7 +333,7 @@ class POCACritic(nn.Module):
             if sequence_length <= 0 or B % sequence_length:
                 raise ValueError("Critic batch must be divisible by sequence_length")
             n_seq = B // sequence_length
-            seq, next_memory = self.lstm(encoding.view(n_seq, sequence_length, self.h_size),
+            seq, next_memory = _lstm(self.lstm, encoding.view(n_seq, sequence_length, self.h_size),
                                          memory if memory is not None else self.initial_state(n_seq, encoding.device))
             encoding = seq.reshape(B, self.hidden_size)
         encoding = torch.cat([encoding, self._norm_agent_count(n_agents, B, encoding.device)], dim=-1)

@@ -307,6 +307,25 @@ __global__ void __launch_bounds__(256) embedding_norm_kernel(int64_t rows, const
     out[i] = make_float4(d.x * rstd, d.y * rstd, d.z * rstd, d.w * rstd);
 }
 
+// One LSTM time step from precomputed gate pre-activations (torch.nn.LSTM gate
+// order i, f, g, o): c' = f c + i g, h' = o tanh(c'). One thread per (row, unit).
+__global__ void __launch_bounds__(256) lstm_cell_kernel(int64_t n, int units, const float* __restrict__ gates,
+                                                        const float* c_prev, float* __restrict__ h_out,
+                                                        float* c_out) {   // c_out may alias c_prev
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n * units) return;
+    const int64_t row = j / units;
+    const int u = (int)(j - row * units);
+    const float* g = gates + row * 4 * units + u;
+    const float ig = 1.0f / (1.0f + expf(-g[0]));
+    const float fg = 1.0f / (1.0f + expf(-g[units]));
+    const float gg = tanhf(g[2 * units]);
+    const float og = 1.0f / (1.0f + expf(-g[3 * units]));
+    const float c = fg * c_prev[j] + ig * gg;
+    c_out[j] = c;
+    h_out[j] = og * tanhf(c);
+}
+
 int g_cus = 0;
 
 }  // namespace
@@ -353,6 +372,18 @@ int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, 
     if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
     embedding_norm_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
         rows, reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out));
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_lstm_cell(int64_t n, int32_t units, const float* gates, const float* c_prev, float* h_out,
+                        float* c_out, void* stream) {
+    if (n < 0 || units < 1) return SWARM_ERR_ARG;
+    if (n == 0) return SWARM_OK;
+    if (!gates || !c_prev || !h_out || !c_out) return SWARM_ERR_ARG;
+    const int64_t blocks = (n * units + 255) / 256;
+    if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
+    lstm_cell_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(n, units, gates, c_prev, h_out,
+                                                                                   c_out);
     return swarm::record_hip_status();
 }
 

@@ -152,3 +152,22 @@ def test_embedding_norm_matches_layer_norm(gpu_device, rows):
     torch.cuda.synchronize()
     torch.testing.assert_close(out, torch.nn.functional.layer_norm(x, (128,)), **TOL)
     assert lib.swarm_rsa_embedding_norm(rows, 64, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), None) == -1
+
+
+@pytest.mark.parametrize("n,inp,units", [(163840, 128, 64), (8192, 128, 64), (5, 7, 3), (1, 128, 64)])
+def test_fused_lstm_step_matches_torch(gpu_device, n, inp, units):
+    """One LSTM step through swarm_lstm_cell (GEMMs + fused cell) against nn.LSTM
+    (MIOpen) on the same GPU; the actor at C3 is 8192 envs x 20 agents."""
+    torch.manual_seed(n)
+    lstm = PN._mlagents_lstm(inp, 2 * units)[0].to(gpu_device)
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.add_(torch.randn_like(p) * 0.1)
+        x = torch.randn(n, 1, inp, device=gpu_device)
+        h = torch.randn(1, n, units, device=gpu_device)
+        c = torch.randn(1, n, units, device=gpu_device) * 2
+        out, (h1, c1) = PN._lstm(lstm, x, (h, c))
+        ref, (rh, rc) = lstm(x, (h, c))
+    torch.testing.assert_close(out, ref, **TOL)
+    torch.testing.assert_close(h1, rh, **TOL)
+    torch.testing.assert_close(c1, rc, **TOL)

@@ -32,6 +32,7 @@ for p in (ROOT, os.path.join(ROOT, "swarmacb-isaaclab_amd")):
 
 from SwarmACB_isaac import ForagingEnvCfg, make  # noqa: E402
 from SwarmACB_isaac.agents import POCARolloutBuffer, POCARolloutCollector  # noqa: E402
+from SwarmACB_isaac.agents import poca_networks as PN  # noqa: E402
 from SwarmACB_isaac.agents.poca_networks import POCACritic, RecurrentDiscreteActor  # noqa: E402
 
 
@@ -134,6 +135,7 @@ def main():
     buf2 = POCARolloutBuffer(args.ref_decisions + 1, E, N, obs_dim=4, act_dim=1, memory_size=64,
                              critic_memory_size=64, device=dev)
     critic.use_fused = False
+    PN.FUSED_LSTM = False
     z = lambda n: torch.zeros(1, n, 64, device=dev)  # noqa: E731
     mem = {"ah": z(E * N), "ac": z(E * N), "ch": z(E), "cc": z(E), "bh": z(E * N), "bc": z(E * N)}
     obs_dict, _ = env2.reset()
