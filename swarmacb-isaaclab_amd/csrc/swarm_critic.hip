@@ -127,24 +127,36 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
             *reinterpret_cast<float4*>(dst) = q4[i];
         }
         __syncthreads();
-        // ---- phase 1: logits of every entity pair and head (within a row group)
-        for (int e = tid; e < ((RSA_ABLATE & 1) ? 0 : NH * R * G); e += NT) {
-            const int h = e / (R * G);
-            const int rem = e - h * R * G;
-            const int qr = rem / G, kr = (qr / G) * G + (rem - qr * G);
-            const float* qp = &Qs[qr * LDSW + h * DH];
-            const float* kp = &Ks[kr * LDSW + h * DH];
-            float acc = 0.0f;
+        // ---- phase 1: logits of every entity pair and head on the matrix cores: per head
+        // S_h = Q_h K_h^T over 16 x 16 tiles of the (padded) R x R pairs. The k order is
+        // permuted as for fc_out (k-step m of lane group kq is feature DH/4 kq + m), so a
+        // lane reads its operands as contiguous float4s. Single-set calls only use the
+        // pairs inside each env's row group.
+        {
+            constexpr int TI = (RMAX + 15) / 16;
+            constexpr int KS = DH / 4;
+            const int rl = lane & 15, kq = lane >> 4;
+            for (int t = tid >> 6; t < ((RSA_ABLATE & 1) ? 0 : NH * TI * TI); t += NT / 64) {
+                const int h = t / (TI * TI), ti = (t / TI) % TI, tj = t % TI;
+                const float* qp = &Qs[min(16 * ti + rl, R - 1) * LDSW + h * DH + KS * kq];
+                const float* kp = &Ks[min(16 * tj + rl, R - 1) * LDSW + h * DH + KS * kq];
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int d = 0; d < DH; d += 4) {
-                const float4 u = *reinterpret_cast<const float4*>(qp + d);
-                const float4 v = *reinterpret_cast<const float4*>(kp + d);
-                acc += u.x * v.x;
-                acc += u.y * v.y;
-                acc += u.z * v.z;
-                acc += u.w * v.w;
+                for (int m = 0; m < KS; m += 4) {
+                    const float4 a = *reinterpret_cast<const float4*>(qp + m);
+                    const float4 bk = *reinterpret_cast<const float4*>(kp + m);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bk.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bk.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bk.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bk.w, acc, 0, 0, 0);
+                }
+                const int kr = 16 * tj + rl;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int qr = 16 * ti + 4 * kq + i;
+                    if (qr < R && kr < R) S[h * SHS + qr * SW + kr] = acc[i] / sqrt_d;
+                }
             }
-            S[h * SHS + qr * SW + kr] = acc / sqrt_d;
         }
         __syncthreads();
         // ---- phase 2: sets in chunks of SETS (waves w and w + 4 own set s0 + w)
