@@ -10,8 +10,9 @@ BASELINE configs (cyclamen / OC: hidden 128, 4 heads, 1 layer, LSTM memory
 1-head variant with the OC2 action-critic state width) it records, as data: the state_dict (every parameter
 perturbed by seeded noise so no bias is zero), random inputs, and the outputs
 of critic_pass / joint_action_pass / all_baselines / baseline (with and
-without LSTM memory, and with sequence_length > 1), plus the attention-pooled
-rows alone. Actors: outputs of Actor, DiscreteActor, RecurrentDiscreteActor.
+without LSTM memory, and with sequence_length > 1), the option-critic
+counterfactuals (all / focal discrete alternatives, focal baselines) for the
+discrete critic, plus the attention-pooled rows alone. Actors: outputs of Actor, DiscreteActor, RecurrentDiscreteActor.
 
 Usage: python tests/golden/critic/make_critic_golden.py
 """
@@ -104,6 +105,23 @@ def main():
                 ms = (mc[0][:, :2].contiguous(), mc[1][:, :2].contiguous())
                 out[prefix + "seq_states"] = seq_states.numpy()
                 out[prefix + "critic_pass_seq"] = crit.critic_pass(seq_states, ms, sequence_length=3).numpy()
+            if disc:
+                # option-critic targets (PN:674-820): counterfactual Q of every discrete alternative,
+                # the focal-agent form with and without memory, and focal baselines. Inputs come from
+                # their own generator so the arrays above keep their values.
+                g2 = torch.Generator().manual_seed(777)
+                focal = torch.randint(0, N, (B,), generator=g2)
+                out[prefix + "action_ids"] = ids.numpy()
+                out[prefix + "focal_ids"] = focal.numpy()
+                out[prefix + "all_cf"] = crit.all_discrete_counterfactual_values(states, ids, A).numpy()
+                out[prefix + "focal_cf"] = crit.focal_discrete_counterfactual_values(states, ids, focal, A).numpy()
+                out[prefix + "focal_baselines"] = crit.focal_baselines(states, actions, focal).numpy()
+                if M:
+                    mf = (torch.randn(1, B, M // 2, generator=g2) * 0.5, torch.randn(1, B, M // 2, generator=g2) * 0.5)
+                    out[prefix + "mem_focal_h"], out[prefix + "mem_focal_c"] = mf[0].numpy(), mf[1].numpy()
+                    out[prefix + "focal_cf_mem"] = crit.focal_discrete_counterfactual_values(
+                        states, ids, focal, A, memory=mf).numpy()
+                    out[prefix + "focal_baselines_mem"] = crit.focal_baselines(states, actions, focal, mf).numpy()
     # actors
     torch.manual_seed(5)
     actor = PN.Actor(24, 2, 64, 2)

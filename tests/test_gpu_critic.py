@@ -171,3 +171,37 @@ def test_fused_lstm_step_matches_torch(gpu_device, n, inp, units):
     torch.testing.assert_close(out, ref, **TOL)
     torch.testing.assert_close(h1, rh, **TOL)
     torch.testing.assert_close(c1, rc, **TOL)
+
+
+def test_option_critic_counterfactuals_fused(gpu_device, fused_calls):
+    """The OC targets (PN:674-820) through the fused kernel against the reference
+    modules' outputs (tests/golden/critic)."""
+    c = IO.critic(G, "cyc_", gpu_device)
+    s, a = IO.t(G, "cyc_states", gpu_device), IO.t(G, "cyc_actions", gpu_device)
+    ids, focal = IO.t(G, "cyc_action_ids", gpu_device), IO.t(G, "cyc_focal_ids", gpu_device)
+    mf = (IO.t(G, "cyc_mem_focal_h", gpu_device), IO.t(G, "cyc_mem_focal_c", gpu_device))
+    with torch.no_grad():
+        close(c.all_discrete_counterfactual_values(s, ids, 6), "cyc_all_cf")
+        close(c.focal_discrete_counterfactual_values(s, ids, focal, 6), "cyc_focal_cf")
+        close(c.focal_baselines(s, a, focal), "cyc_focal_baselines")
+        close(c.focal_discrete_counterfactual_values(s, ids, focal, 6, memory=mf), "cyc_focal_cf_mem")
+        close(c.focal_baselines(s, a, focal, mf), "cyc_focal_baselines_mem")
+    assert fused_calls and set(fused_calls) == {0}
+
+
+def test_focal_counterfactuals_at_c4_size(gpu_device):
+    """DirGate cyclamen OC (C4): 2048 envs per GPU, 6 options; fused vs PyTorch path."""
+    torch.manual_seed(4)
+    E, N, A = 2048, 20, 6
+    c = PN.POCACritic(5, A, N, 128, 4, 1, memory_size=128).to(gpu_device).eval()
+    with torch.no_grad():
+        for p in c.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+        s = torch.randn(E, N, 5, device=gpu_device)
+        ids = torch.randint(0, A, (E, N), device=gpu_device)
+        focal = torch.randint(0, N, (E,), device=gpu_device)
+        mem = (torch.randn(1, E, 64, device=gpu_device), torch.randn(1, E, 64, device=gpu_device))
+        fused = c.focal_discrete_counterfactual_values(s, ids, focal, A, memory=mem)
+        c.use_fused = False
+        ref = c.focal_discrete_counterfactual_values(s, ids, focal, A, memory=mem)
+    torch.testing.assert_close(fused, ref, **TOL)

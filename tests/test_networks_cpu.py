@@ -83,3 +83,22 @@ def test_memory_size_validation_and_checkpoint_helper():
         PN._mlagents_lstm(16, 63)
     assert PN.checkpoint_memory_size({"memory_size": 64}) == 128
     assert PN.checkpoint_memory_size({"memory_size": 128, "memory_size_semantics": "mlagents_total"}) == 128
+
+
+def test_option_critic_counterfactuals_match_reference():
+    """all / focal discrete counterfactual Q and focal baselines (PN:674-820) of the
+    discrete cyclamen critic, with and without LSTM memory, on the PyTorch path."""
+    G = IO.load()
+    c = IO.critic(G, "cyc_")
+    s, a = IO.t(G, "cyc_states"), IO.t(G, "cyc_actions")
+    ids, focal = IO.t(G, "cyc_action_ids"), IO.t(G, "cyc_focal_ids")
+    mf = (IO.t(G, "cyc_mem_focal_h"), IO.t(G, "cyc_mem_focal_c"))
+    tol = dict(rtol=1e-5, atol=1e-5)
+    with torch.no_grad():
+        got = {"all_cf": c.all_discrete_counterfactual_values(s, ids, 6),
+               "focal_cf": c.focal_discrete_counterfactual_values(s, ids, focal, 6),
+               "focal_baselines": c.focal_baselines(s, a, focal),
+               "focal_cf_mem": c.focal_discrete_counterfactual_values(s, ids, focal, 6, memory=mf),
+               "focal_baselines_mem": c.focal_baselines(s, a, focal, mf)}
+    for k, v in got.items():
+        np.testing.assert_allclose(v.numpy(), G["cyc_" + k], err_msg=k, **tol)
