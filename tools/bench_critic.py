@@ -92,7 +92,8 @@ def main():
     print(json.dumps({"stage": "rsa_pool_kernel", "ms": sec * 1e3, "algorithmic_flops": flops,
                       "roofline": {"bound": "mfma", "achieved": flops / sec / 1e12, "peak": MFMA_F32_PEAK,
                                    "unit": "TFLOP/s", "frac": flops / sec / 1e12 / MFMA_F32_PEAK,
-                                   "mfma_share_of_flops": fc_flops / (fc_flops + other)},
+                                   # logits, P.V and fc_out all run on v_mfma_f32_16x16x4_f32
+                                   "mfma_share_of_flops": 1.0},
                       "config": cfg}), flush=True)
 
     # ---- what the rollout calls per decision (no_grad), fused vs PyTorch path
