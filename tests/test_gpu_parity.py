@@ -333,3 +333,29 @@ def test_full_size_homing_properties(gpu_device):
     assert (sd >= 0.035).all(), sd.min()
     assert (eng.episode_length.cpu().numpy() == 0).all()
     eng.close()
+
+
+def test_maximum_env_count_indexing(gpu_device):
+    """The largest batch the 32-bit element indexing admits (E x 20 x 24 < 2^31:
+    4,473,924 envs, 89.5 M robots): its last envs equal the same envs run as a
+    4-env shard (env_offset), bit for bit; one env more is refused."""
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    emax = ((1 << 31) - 1) // (20 * 24)
+    with pytest.raises(RuntimeError):
+        SwarmEngine("homing", "isaac", emax + 1, 20, 24, False, 1200, 1, 0, 5, gpu_device)
+    big = SwarmEngine("homing", "isaac", emax, 20, 24, False, 1200, 1, 0, 5, gpu_device)
+    small = SwarmEngine("homing", "isaac", 4, 20, 24, False, 1200, 1, emax - 4, 5, gpu_device)
+    ob, _, _ = big.reset()
+    os_, _, _ = small.reset()
+    assert torch.equal(ob[-4:], os_)
+    g = torch.Generator(device=gpu_device).manual_seed(3)
+    for _ in range(2):
+        a = (torch.randn(emax, 20, 2, device=gpu_device, generator=g).clamp_(-3, 3) / 3).contiguous()
+        ob, rb, tb = big.step(a, 5)
+        os_, rs, ts = small.step(a[-4:].contiguous(), 5)
+        assert torch.equal(ob[-4:], os_) and torch.equal(rb[-4:], rs) and torch.equal(tb[-4:], ts)
+    assert torch.equal(big.x.view(-1)[-80:], small.x.view(-1)) and torch.equal(big.y.view(-1)[-80:], small.y.view(-1))
+    assert torch.isfinite(ob).all()
+    big.close()
+    small.close()
