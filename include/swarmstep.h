@@ -150,6 +150,11 @@ int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float*
  * a device sync). Call after writing state->episode_length from the host. */
 int32_t swarm_sync_episode_lengths(swarm_handle_t* h, const int32_t* host_lengths);
 int64_t swarm_tick(const swarm_handle_t* h);
+/* Bit s set: in substep s of the last swarm_step some env reached max_episode_length (from the
+ * host mirror, no device sync; -1 for a null handle). A caller skips work that only time-outs
+ * need, e.g. the terminal-state critic value of poca_trainer.py:575-583 (it is multiplied by the
+ * time-out flags, so it is 0 for every env when no bit is set). */
+int64_t swarm_last_timeouts(const swarm_handle_t* h);
 
 /* Behaviour-FSM packing helpers (host). Unpacked fields follow
  * BehaviorModules (behavior_modules.py:141-153). */

@@ -116,6 +116,7 @@ class POCARolloutCollector:
         E, N = self.num_envs, self.num_agents
         self._obs = torch.zeros(E, N, buffer.obs_dim, device=self.device)
         self._rew = torch.zeros(E, device=self.device)
+        self._zero_values = torch.zeros(E, device=self.device)
         self._trunc = torch.zeros(E, dtype=torch.uint8, device=self.device)
         if recurrent:
             ah, ch = actor.hidden_size, critic.hidden_size
@@ -195,11 +196,17 @@ class POCARolloutCollector:
             obs_out = buf.obs[t + 1] if t + 1 < buf.horizon else self._obs
             obs_next, rew, trunc = self.env.step_decision(env_actions, dp, out=(obs_out, self._rew, self._trunc))
 
-            terminal = self.env.completed_terminal_critic_state
-            if self.recurrent:
-                tv = self.critic.critic_pass(terminal, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
+            # the terminal-state value is multiplied by the time-out flags (PT:575-583): when the
+            # host mirror says no env timed out in this decision it is 0 for every env, and the
+            # critic pass is skipped (critic_pass with memory does not advance the memory)
+            if self.env.engine.last_timeouts:
+                terminal = self.env.completed_terminal_critic_state
+                if self.recurrent:
+                    tv = self.critic.critic_pass(terminal, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
+                else:
+                    tv = self.critic.critic_pass(terminal).squeeze(-1)
             else:
-                tv = self.critic.critic_pass(terminal).squeeze(-1)
+                tv = self._zero_values
             mems = []
             if self.recurrent:
                 mems = [(self.actor_memory_h, N), (self.actor_memory_c, N), (self.critic_memory_h, 1),

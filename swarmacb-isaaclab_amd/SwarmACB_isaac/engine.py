@@ -168,6 +168,11 @@ class SwarmEngine:
     def tick(self) -> int:
         return int(self.lib.swarm_tick(self.handle))
 
+    @property
+    def last_timeouts(self) -> int:
+        """Bit s: some env timed out in substep s of the last step() (host mirror, no sync)."""
+        return int(self.lib.swarm_last_timeouts(self.handle))
+
     def close(self):
         if getattr(self, "handle", None):
             self.lib.swarm_destroy(self.handle)

@@ -69,6 +69,7 @@ struct swarm_handle {
     bool lens_exact = true;     // lens[] matches the mirror
     uint8_t* d_mask = nullptr;  // E-byte device scratch for reset masks
     bool was_reset = false;
+    uint64_t last_timeouts = 0;  // substeps of the last swarm_step in which some env timed out
 };
 
 namespace {
@@ -170,6 +171,8 @@ int32_t swarm_sync_episode_lengths(swarm_handle_t* h, const int32_t* host_length
 
 int64_t swarm_tick(const swarm_handle_t* h) { return h ? (int64_t)h->tick : -1; }
 
+int64_t swarm_last_timeouts(const swarm_handle_t* h) { return h ? (int64_t)h->last_timeouts : -1; }
+
 int32_t swarm_reset(swarm_handle_t* h, const swarm_state_t* state, const uint8_t* env_mask_host,
                     const swarm_outputs_t* out, const swarm_replay_t* replay, void* stream) {
     if (!h || !state_ok(state) || !out || !out->obs) return SWARM_ERR_ARG;
@@ -223,6 +226,7 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     for (int s = 0; s < n_substeps; ++s) {
         if (h->mirror.step()) reset_any |= 1ull << s;
     }
+    h->last_timeouts = reset_any;
     h->lens_exact = h->mirror.buckets.size() <= 1;
     if (h->lens_exact && !h->mirror.buckets.empty())
         h->lens.assign(h->p.num_envs, (int32_t)(h->mirror.buckets.begin()->first + h->mirror.offset));

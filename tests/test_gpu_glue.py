@@ -296,3 +296,19 @@ def test_record_learned_option_critic_slabs(gpu_device):
         d = done.repeat_interleave(r)
         assert (m[0, d] == 0).all() and torch.equal(m[0, ~d], b[0, ~d])
     assert (options[done] == -1).all() and torch.equal(options[~done], opt_before[~done])
+
+
+def test_last_timeouts_mask(gpu_device):
+    """swarm_last_timeouts: the substeps of the last launch in which some env timed out."""
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    eng = SwarmEngine("homing", "isaac", 8, 20, 24, False, 12, 1, 0, 1, gpu_device)
+    eng.reset()
+    a = torch.zeros(8, 20, 2, device=gpu_device)
+    eng.step(a, 5)
+    assert eng.last_timeouts == 0                  # steps 1-5
+    eng.step(a, 5)
+    assert eng.last_timeouts == 0                  # steps 6-10
+    _, _, tr = eng.step(a, 5)
+    assert eng.last_timeouts == 1 << 1 and bool(tr.all())   # step 12 is substep 1 of steps 11-15
+    eng.close()
