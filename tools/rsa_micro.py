@@ -1,3 +1,5 @@
+"""Microbenchmark of swarm_rsa_pool (both modes, C3 and neighbouring batch sizes) on the GPU box:
+   python3 tools/rsa_micro.py  ->  "mode envs ms" lines."""
 import ctypes as C, sys, torch
 sys.path.insert(0, "swarmacb-isaaclab_amd")
 from SwarmACB_isaac import _native
