@@ -125,6 +125,18 @@ class POCARolloutCollector:
             self.critic_memory_h, self.critic_memory_c = z(1, E, ch), z(1, E, ch)
             self.baseline_memory_h, self.baseline_memory_c = z(1, E * N, ch), z(1, E * N, ch)
 
+    def _value_and_baselines(self, states, actions, memory=None, baseline_memory=None):
+        """V(s) and all baselines of one decision; through the critic's shared-projection
+        value_and_baselines when it has one (POCACritic), else the reference's two calls
+        (poca_trainer.py:519-548)."""
+        fn = getattr(self.critic, "value_and_baselines", None)
+        if fn is not None:
+            return fn(states, actions, memory, baseline_memory)
+        if memory is None and baseline_memory is None:
+            return (self.critic.critic_pass(states), None), (self.critic.all_baselines(states, actions), None)
+        return (self.critic.critic_pass(states, memory, return_memory=True),
+                self.critic.all_baselines(states, actions, baseline_memory, return_memory=True))
+
     def _encode_actions_for_critic(self, actions):
         """poca_trainer.py:406-419."""
         if self.discrete:
@@ -165,17 +177,15 @@ class POCARolloutCollector:
                 cmh, cmc = self.critic_memory_h.squeeze(0).clone(), self.critic_memory_c.squeeze(0).clone()
                 bmh = self.baseline_memory_h.squeeze(0).view(E, N, -1).clone()
                 bmc = self.baseline_memory_c.squeeze(0).view(E, N, -1).clone()
-                team_val, ncm = self.critic.critic_pass(critic_state, (self.critic_memory_h, self.critic_memory_c),
-                                                        return_memory=True)
-                baselines, nbm = self.critic.all_baselines(
-                    critic_state, critic_actions, (self.baseline_memory_h, self.baseline_memory_c),
-                    return_memory=True)
+                (team_val, ncm), (baselines, nbm) = self._value_and_baselines(
+                    critic_state, critic_actions, (self.critic_memory_h, self.critic_memory_c),
+                    (self.baseline_memory_h, self.baseline_memory_c))
                 self.critic_memory_h, self.critic_memory_c = ncm[0].detach(), ncm[1].detach()
                 self.baseline_memory_h, self.baseline_memory_c = nbm[0].detach(), nbm[1].detach()
                 team_val = team_val.squeeze(-1)
             else:
-                team_val = self.critic.critic_pass(critic_state).squeeze(-1)
-                baselines = self.critic.all_baselines(critic_state, critic_actions)
+                (team_val, _), (baselines, _) = self._value_and_baselines(critic_state, critic_actions)
+                team_val = team_val.squeeze(-1)
 
             env_actions = all_actions if self.discrete else all_actions.clamp(-3, 3) / 3
             # store the pre-decision row, then one launch for the whole decision period

@@ -255,9 +255,12 @@ class ResidualSelfAttention(nn.Module):
         return (out * keep).sum(dim=1) / (keep.sum(dim=1) + self.EPSILON)
 
 
-def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode: int, n: int) -> torch.Tensor:
+def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode, n: int):
     """Attention pooling of the entity sets of every env through swarm_rsa_pool.
-    rows: (B, R, h) embedded entities (R = n, or 2n for the baseline sets)."""
+    rows: (B, R, h) embedded entities (R = n, or 2n for the baseline sets). `mode`
+    may be a tuple of modes over the same rows: the LayerNorm and projection run
+    once and a tuple of pooled tensors is returned."""
+    modes = mode if isinstance(mode, tuple) else (mode,)
     B = rows.shape[0]
     rows = rows.contiguous()
     x = torch.empty_like(rows)
@@ -269,14 +272,17 @@ def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode: int, n: in
     w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
     b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
     qkv = torch.nn.functional.linear(x, w, b).contiguous()
-    n_sets = n if mode == _native.RSA_BASELINES else 1
-    pooled = torch.empty(B * n_sets, attn.embed_dim, dtype=torch.float32, device=rows.device)
     wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
-    rc = lib.swarm_rsa_pool(mode, B, n, attn.num_heads, attn.embed_dim, C.c_void_p(x.data_ptr()),
-                            C.c_void_p(qkv.data_ptr()), C.c_void_p(wo.data_ptr()), C.c_void_p(bo.data_ptr()),
-                            C.c_void_p(pooled.data_ptr()), stream)
-    _native.check(rc, "swarm_rsa_pool")
-    return pooled
+    out = []
+    for m in modes:
+        n_sets = n if m == _native.RSA_BASELINES else 1
+        pooled = torch.empty(B * n_sets, attn.embed_dim, dtype=torch.float32, device=rows.device)
+        rc = lib.swarm_rsa_pool(m, B, n, attn.num_heads, attn.embed_dim, C.c_void_p(x.data_ptr()),
+                                C.c_void_p(qkv.data_ptr()), C.c_void_p(wo.data_ptr()), C.c_void_p(bo.data_ptr()),
+                                C.c_void_p(pooled.data_ptr()), stream)
+        _native.check(rc, "swarm_rsa_pool")
+        out.append(pooled)
+    return tuple(out) if isinstance(mode, tuple) else out[0]
 
 
 class POCACritic(nn.Module):
@@ -415,6 +421,23 @@ class POCACritic(nn.Module):
         return self.baseline(all_states[rows, focal], all_states[keep].view(B, N - 1, self.state_dim),
                              all_actions[keep].view(B, N - 1, self.act_dim), memory, sequence_length,
                              return_memory)
+
+    def value_and_baselines(self, all_states, all_actions, memory=None, baseline_memory=None):
+        """(critic_pass(states, memory, return_memory=True), all_baselines(states, actions,
+        baseline_memory, return_memory=True)) — the two critic calls of a rollout decision
+        (poca_trainer.py:519-548). On the fused path the state-entity rows are embedded,
+        normalised and projected once for both (swarm_rsa_pool SINGLE_OF_PAIRS + BASELINES)."""
+        B, N, _ = all_states.shape
+        if not self._fused(all_states, N):
+            return (self.critic_pass(all_states, memory, return_memory=True),
+                    self.all_baselines(all_states, all_actions, baseline_memory, return_memory=True))
+        obs_emb = self.obs_entity_enc(all_states)
+        act_emb = self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1))
+        pooled_v, pooled_b = _fused_rsa(self.self_attn, torch.cat([obs_emb, act_emb], dim=1),
+                                        (_native.RSA_SINGLE_OF_PAIRS, _native.RSA_BASELINES), N)
+        value = self._value_tail(pooled_v, N, memory, 1, True)
+        bl, next_bm = self._value_tail(pooled_b, N, baseline_memory, 1, True)
+        return value, (bl.squeeze(-1).reshape(B, N), next_bm)
 
     def all_baselines(self, all_states, all_actions, memory=None, sequence_length: int = 1,
                       return_memory: bool = False):

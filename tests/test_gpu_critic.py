@@ -117,7 +117,7 @@ def test_rejects_unsupported_shapes(gpu_device):
     assert lib.swarm_rsa_pool(0, 1, 21, 4, 128, p, p, p, p, p, None) == -1   # N > 20
     assert lib.swarm_rsa_pool(0, 1, 20, 8, 128, p, p, p, p, p, None) == -1   # 8 heads
     assert lib.swarm_rsa_pool(0, 1, 20, 4, 256, p, p, p, p, p, None) == -1   # hidden 256
-    assert lib.swarm_rsa_pool(2, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode
+    assert lib.swarm_rsa_pool(3, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode
 
 
 @pytest.mark.parametrize("B,N,heads", [(1, 20, 4), (7, 20, 2), (5, 13, 4), (9, 3, 1), (2, 1, 4)])
@@ -205,3 +205,30 @@ def test_focal_counterfactuals_at_c4_size(gpu_device):
         c.use_fused = False
         ref = c.focal_discrete_counterfactual_values(s, ids, focal, A, memory=mem)
     torch.testing.assert_close(fused, ref, **TOL)
+
+
+@pytest.mark.parametrize("memory", [False, True])
+def test_value_and_baselines_shares_rows(gpu_device, fused_calls, memory):
+    """The rollout's pair of critic calls on one projection pass (SINGLE_OF_PAIRS +
+    BASELINES) equals critic_pass and all_baselines called separately."""
+    torch.manual_seed(7)
+    E, N = 1027, 20
+    c = PN.POCACritic(5, 6, N, 128, 4, 1, memory_size=128 if memory else 0).to(gpu_device).eval()
+    with torch.no_grad():
+        for p in c.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+        s = torch.randn(E, N, 5, device=gpu_device)
+        a = torch.nn.functional.one_hot(torch.randint(0, 6, (E, N), device=gpu_device), 6).float()
+        mc = mb = None
+        if memory:
+            mc = (torch.randn(1, E, 64, device=gpu_device), torch.randn(1, E, 64, device=gpu_device))
+            mb = (torch.randn(1, E * N, 64, device=gpu_device), torch.randn(1, E * N, 64, device=gpu_device))
+        (v, vm), (b, bm) = c.value_and_baselines(s, a, mc, mb)
+        assert fused_calls == [(2, 1)]  # one shared projection pass, both kernel modes
+        rv, rvm = c.critic_pass(s, mc, return_memory=True)
+        rb, rbm = c.all_baselines(s, a, mb, return_memory=True)
+    torch.testing.assert_close(v, rv, **TOL)
+    torch.testing.assert_close(b, rb, **TOL)
+    if memory:
+        torch.testing.assert_close(vm[0], rvm[0], **TOL)
+        torch.testing.assert_close(bm[1], rbm[1], **TOL)
