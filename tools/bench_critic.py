@@ -102,7 +102,12 @@ def main():
             crit.critic_pass(s, mem_c, return_memory=True)
             crit.all_baselines(s, a, mem_b, return_memory=True)
 
-    fused = timed(rollout_calls, args.reps)
+    def rollout_calls_shared():
+        with torch.no_grad():
+            crit.value_and_baselines(s, a, mem_c, mem_b)
+
+    separate = timed(rollout_calls, args.reps)
+    fused = timed(rollout_calls_shared, args.reps)   # what the collector calls (shared projection)
     crit.use_fused = False
     torch_gpu = timed(rollout_calls, max(3, args.reps // 4))
     crit.use_fused = True
@@ -117,7 +122,8 @@ def main():
         cpu.critic_pass(sc, (mem_c[0][:, :ce].cpu(), mem_c[1][:, :ce].cpu()), return_memory=True)
         cpu.all_baselines(sc, ac, (mem_b[0][:, :ce * N].cpu(), mem_b[1][:, :ce * N].cpu()), return_memory=True)
         cpu_s = (time.perf_counter() - t0) * E / ce
-    print(json.dumps({"stage": "critic_rollout_calls", "ms": fused * 1e3, "torch_path_gpu_ms": torch_gpu * 1e3,
+    print(json.dumps({"stage": "critic_rollout_calls", "ms": fused * 1e3, "separate_calls_ms": separate * 1e3,
+                      "torch_path_gpu_ms": torch_gpu * 1e3,
                       "speedup_vs_torch_gpu": torch_gpu / fused,
                       "cpu_baseline": {"ms": cpu_s * 1e3, "kind": "port", "cores": torch.get_num_threads(),
                                        "sample": f"same module, PyTorch path on host CPU, {ce} envs, scaled x{E / ce:g}"},
