@@ -153,10 +153,11 @@ class POCARolloutCollector:
             if t >= buf.horizon:
                 raise RuntimeError(buf._full_message)
             flat_obs = obs.reshape(E * N, -1)
-            memory_h = memory_c = None
             if self.recurrent:
-                memory_h = self.actor_memory_h.squeeze(0).view(E, N, -1).clone()
-                memory_c = self.actor_memory_c.squeeze(0).view(E, N, -1).clone()
+                # the pre-decision memories go straight into buffer row t (nothing reads the row
+                # before the step, and the networks return new memory tensors)
+                buf.memory_h[t].copy_(self.actor_memory_h.squeeze(0).view(E, N, -1))
+                buf.memory_c[t].copy_(self.actor_memory_c.squeeze(0).view(E, N, -1))
                 logits, nm = self.actor.step(flat_obs, (self.actor_memory_h, self.actor_memory_c))
                 self.actor_memory_h, self.actor_memory_c = nm[0].detach(), nm[1].detach()
                 dist = torch.distributions.Categorical(logits=logits)
@@ -172,11 +173,12 @@ class POCARolloutCollector:
             critic_state = self.env.engine.critic_state(out=buf.critic_states[t]) \
                 if hasattr(self.env, "engine") else self.env.get_critic_state()
             critic_actions = self._encode_actions_for_critic(all_actions)
-            cmh = cmc = bmh = bmc = None
             if self.recurrent:
-                cmh, cmc = self.critic_memory_h.squeeze(0).clone(), self.critic_memory_c.squeeze(0).clone()
-                bmh = self.baseline_memory_h.squeeze(0).view(E, N, -1).clone()
-                bmc = self.baseline_memory_c.squeeze(0).view(E, N, -1).clone()
+                if buf.critic_memory_size > 0:
+                    buf.critic_memory_h[t].copy_(self.critic_memory_h.squeeze(0))
+                    buf.critic_memory_c[t].copy_(self.critic_memory_c.squeeze(0))
+                    buf.baseline_memory_h[t].copy_(self.baseline_memory_h.squeeze(0).view(E, N, -1))
+                    buf.baseline_memory_c[t].copy_(self.baseline_memory_c.squeeze(0).view(E, N, -1))
                 (team_val, ncm), (baselines, nbm) = self._value_and_baselines(
                     critic_state, critic_actions, (self.critic_memory_h, self.critic_memory_c),
                     (self.baseline_memory_h, self.baseline_memory_c))
@@ -197,11 +199,6 @@ class POCARolloutCollector:
             buf.log_probs[t] = all_log_probs
             buf.team_values[t] = team_val
             buf.baselines[t] = baselines
-            if self.recurrent:
-                buf.memory_h[t], buf.memory_c[t] = memory_h, memory_c
-                if buf.critic_memory_size > 0:
-                    buf.critic_memory_h[t], buf.critic_memory_c[t] = cmh, cmc
-                    buf.baseline_memory_h[t], buf.baseline_memory_c[t] = bmh, bmc
             # the step writes the next decision's observation straight into buffer row t+1
             obs_out = buf.obs[t + 1] if t + 1 < buf.horizon else self._obs
             obs_next, rew, trunc = self.env.step_decision(env_actions, dp, out=(obs_out, self._rew, self._trunc))
