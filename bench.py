@@ -52,7 +52,10 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo")
     ap.add_argument("--layout", type=int, default=0,
                     help="kernel work layout (1/2/4 waves per 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget per leg (0 = skip)")
+    ap.add_argument("--prewarm", type=float, default=1.0,
+                    help="seconds of untimed step launches on a scratch engine before the warm-up "
+                         "(brings the GPU to steady clocks; steps/warmup semantics unchanged)")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
@@ -64,20 +67,28 @@ def parse():
     return args
 
 
-def cpu_baseline(budget_s: float, envs: int) -> dict | None:
-    """Reference-equivalent CPU step (the C restatement in oracle/, 1 thread) on a bounded sample."""
-    if budget_s <= 0:
-        return None
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_worker(args):
+    """One process of the CPU baseline: its own oracle instance stepping `E` envs for `budget_s`."""
+    E, budget_s, seed = args
     import numpy as np
 
     from oracle import oracle as O
 
-    O.build()
-    E = min(envs, 1024)
     env = O.OracleEnv("homing", "isaac", E, N_AGENTS, 24, False, 1200)
-    O.seed(0)
+    O.seed(seed)
     env.reset_all()
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     steps, t0 = 0, time.perf_counter()
     while True:
         a = (np.clip(rng.normal(size=(E, N_AGENTS, 2)), -3, 3) / 3).astype(np.float32)
@@ -86,11 +97,38 @@ def cpu_baseline(budget_s: float, envs: int) -> dict | None:
             steps += 1
         el = time.perf_counter() - t0
         if el >= budget_s:
-            break
-    return {"value": E * N_AGENTS * steps / el, "unit": "agent-steps/s", "cores": 1, "kind": "port",
+            return E * N_AGENTS * steps, el
+
+
+def cpu_baseline(budget_s: float, envs: int) -> dict | None:
+    """Reference-equivalent CPU step (the C restatement in oracle/) on a bounded sample:
+    1 thread, then one process per host core (capped at the box's 16-core share),
+    each stepping its own slice of envs; the all-cores figure is `value`."""
+    if budget_s <= 0:
+        return None
+    import multiprocessing as mp
+
+    from oracle import oracle as O
+
+    O.build()
+    E = min(envs, 1024)
+    n1, el1 = _oracle_worker((E, budget_s, 0))
+    one = n1 / el1
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+    per = max(1, E // cores)
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(_oracle_worker, [(per, budget_s, 1 + k) for k in range(cores)])
+    allv = sum(n / el for n, el in res)
+    return {"value": allv, "unit": "agent-steps/s", "cores": cores, "kind": "port",
+            "one_thread": one, "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
             "sample": f"oracle/swarm_oracle.c (C restatement of the reference step, pinned by tests/golden) "
-                      f"Homing dandelion isaac profile, {E} envs x 20 e-pucks x {steps} env.steps "
-                      f"({el:.1f} s, 1 thread, host CPU)"}
+                      f"Homing dandelion isaac profile, policy N(0,1)->clamp/3 per 5-step decision; "
+                      f"1 thread: {E} envs x 20 e-pucks for {el1:.1f} s = {one:.4g} agent-steps/s; "
+                      f"all cores: {cores} processes x {per} envs x 20 e-pucks for {budget_s:.0f} s each"}
 
 
 def load_pmc(envs: int, sub: int) -> dict:
@@ -106,6 +144,24 @@ def load_pmc(envs: int, sub: int) -> dict:
     if d.get("envs") != envs or d.get("substeps") != sub:
         return {}
     return d
+
+
+def prewarm(seconds: float, E: int, dp: int, dev) -> float:
+    """Untimed launches of the same step on a scratch engine for `seconds` (clock ramp-up)."""
+    if seconds <= 0:
+        return 0.0
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, 0, 12345, dev)
+    out = eng.reset()
+    a = torch.zeros(E, N_AGENTS, 2, device=dev)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            eng.step(a, dp, out=out)
+        torch.cuda.synchronize(dev)
+    eng.close()
+    return time.perf_counter() - t0
 
 
 def main():
@@ -148,6 +204,7 @@ def main():
     from SwarmACB_isaac.shard import EnvShard, max_over_ranks
 
     E, dp = args.envs, args.decision_period
+    prewarm_s = prewarm(args.prewarm, E, dp, dev)
     shard = EnvShard.weak(E, rank, world)     # weak scaling: E envs per GPU, keyed by global env id
     eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, shard.env_offset, args.seed, dev,
                       layout=args.layout or None)
@@ -197,7 +254,8 @@ def main():
             peak = VALU_PEAK_LANE_OPS
             valu = {"achieved": lane_ops / avg_kernel_s / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s",
                     "frac": lane_ops / avg_kernel_s / peak,
-                    "valu_insts_per_launch": pmc["valu_insts_per_launch"]}
+                    "valu_insts_per_launch": pmc["valu_insts_per_launch"],
+                    "valu_insts_source": "profiles/pmc_traffic.json (SQ_INSTS_VALU pass); not measured in this process"}
         line = {
             "metric": METRIC,
             "value": value,
@@ -205,6 +263,7 @@ def main():
             "n_gpus": world,
             "steps": steps,
             "warmup": n_warm * dp,
+            "prewarm_s": prewarm_s,
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
@@ -229,6 +288,8 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of "
+                                  "this workload, tools/pmc.sh); not measured in this process" if traffic else None,
                 "traffic_per_agent_step": (traffic / (E * N_AGENTS * dp)) if traffic else None,
                 "valu": valu,
                 "kernel": "step_kernel<HOMING,ISAAC,continuous,N=20,W>",

@@ -75,6 +75,27 @@ def _ptr(a, ctype):
     return a.ctypes.data_as(C.POINTER(ctype))
 
 
+def _draws_struct(draws: dict | None):
+    """(kept arrays, _Draws) for an or_draws argument (None -> oracle's own generator)."""
+    keep = []
+    if draws is None:
+        return keep, None
+
+    def arr(k, dt):
+        v = draws.get(k)
+        if v is None:
+            return None
+        v = np.ascontiguousarray(np.asarray(v), dt)
+        keep.append(v)
+        return v
+    ro, rd = arr("rab_u_obs", np.float32), arr("rab_u_dispatch", np.float32)
+    tu, tp = arr("turns", np.int32), arr("turn_present", np.int32)
+    su, sy = arr("spawn_u", np.float32), arr("spawn_yaw_u", np.float32)
+    d = _Draws(_ptr(ro, C.c_float), _ptr(rd, C.c_float), _ptr(tu, C.c_int32), _ptr(tp, C.c_int32),
+               _ptr(su, C.c_float), int(draws.get("spawn_k", 0)), _ptr(sy, C.c_float))
+    return keep, d
+
+
 class OracleEnv:
     """Holds an oracle state (numpy arrays, reference tensor layout)."""
 
@@ -120,21 +141,7 @@ class OracleEnv:
             else:
                 act_c = a.astype(np.float32).reshape(E, N, 2)
         ovr = None if override is None else np.ascontiguousarray(override, np.float32)
-        keep = []
-        d = None
-        if draws is not None:
-            def arr(k, dt):
-                v = draws.get(k)
-                if v is None:
-                    return None
-                v = np.ascontiguousarray(np.asarray(v), dt)
-                keep.append(v)
-                return v
-            ro, rd = arr("rab_u_obs", np.float32), arr("rab_u_dispatch", np.float32)
-            tu, tp = arr("turns", np.int32), arr("turn_present", np.int32)
-            su, sy = arr("spawn_u", np.float32), arr("spawn_yaw_u", np.float32)
-            d = _Draws(_ptr(ro, C.c_float), _ptr(rd, C.c_float), _ptr(tu, C.c_int32), _ptr(tp, C.c_int32),
-                       _ptr(su, C.c_float), int(draws.get("spawn_k", 0)), _ptr(sy, C.c_float))
+        keep, d = _draws_struct(draws)
         obs = np.zeros((E, N, self.obs_dim), np.float32)
         rew = np.zeros(E, np.float32)
         tr = np.zeros(E, np.int32)
@@ -162,6 +169,18 @@ class OracleEnv:
             raise RuntimeError(f"oracle or_reset_all failed rc={rc}")
         return obs
 
+    def reset_envs(self, mask, draws: dict | None = None):
+        """_reset_idx(mask) then observations of all envs (isaac profile)."""
+        obs = np.zeros((self.E, self.N, self.obs_dim), np.float32)
+        m = np.ascontiguousarray(np.asarray(mask, np.uint8).reshape(self.E))
+        keep, d = _draws_struct(draws)
+        st = self._state_struct()
+        rc = lib().or_reset_idx(C.byref(self.cfg), C.byref(st), _ptr(m, C.c_uint8),
+                                C.byref(d) if d is not None else None, _ptr(obs, C.c_float))
+        if rc != 0:
+            raise RuntimeError(f"oracle or_reset_idx failed rc={rc}")
+        return obs
+
     def critic_state(self):
         out = np.zeros((self.E, self.N, 5), np.float32)
         lib().or_critic_state(C.byref(self.cfg), _ptr(self.s["pos"], C.c_float), _ptr(self.s["yaw"], C.c_float),
@@ -182,6 +201,39 @@ class libm_perturb:
     def __exit__(self, *exc):
         lib().or_set_libm_perturb(0)
         return False
+
+
+def philox_draws(seed: int, env_offset: int, E: int, N: int, tick: int, profile: str = "isaac", parts: int = 3,
+                 spawn_k: int = 0, dispatch: bool = False) -> dict:
+    """The production HIP kernel's Philox draws of one tick (or_philox_draws), as an
+    OracleEnv.step `draws` dict. parts: 3 = the step kernel's layout 103, 1 = reset kernel."""
+    EN = E * N
+    rab = np.zeros((E, N, N), np.float32)
+    rd = np.zeros((E, N, N), np.float32) if dispatch else None
+    turns = np.zeros((3, E, N), np.int32)
+    if profile == "isaac":
+        su = np.zeros((spawn_k, E, N, 2), np.float32) if spawn_k else None
+        sy = np.zeros((E, N), np.float32) if spawn_k else None
+    else:
+        su, sy = np.zeros((3, E, N), np.float32), None
+    f = lib().or_philox_draws
+    f.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
+                  C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_int32), C.POINTER(C.c_float),
+                  C.POINTER(C.c_float)]
+    rc = f(int(seed) & (2**64 - 1), int(env_offset), E, N, parts, int(tick), PROFILE_IDS[profile], int(spawn_k),
+           _ptr(rab, C.c_float), _ptr(rd, C.c_float), _ptr(turns, C.c_int32), _ptr(su, C.c_float),
+           _ptr(sy, C.c_float))
+    if rc != 0:
+        raise RuntimeError(f"or_philox_draws failed rc={rc}")
+    d = {"rab_u_obs": rab, "turns": turns, "turn_present": np.ones(3, np.int32)}
+    if rd is not None:
+        d["rab_u_dispatch"] = rd
+    if su is not None:
+        d["spawn_u"] = su
+        d["spawn_k"] = spawn_k if profile == "isaac" else 3
+    if sy is not None:
+        d["spawn_yaw_u"] = sy
+    return d
 
 
 def seed(s: int):

@@ -1058,11 +1058,11 @@ void or_rng_uniform(float* out, int n) {
     for (int k = 0; k < n; k++) out[k] = mt_uniform();
 }
 
-int or_reset_all(const or_cfg* c, or_state* st, const or_draws* d, float* obs) {
+int or_reset_idx(const or_cfg* c, or_state* st, const uint8_t* env_mask, const or_draws* d, float* obs) {
     geom g;
     build_geom(c, &g);
     uint8_t* mask = (uint8_t*)malloc((size_t)c->E);
-    for (int e = 0; e < c->E; e++) mask[e] = 1;
+    for (int e = 0; e < c->E; e++) mask[e] = env_mask ? (env_mask[e] != 0) : 1;
     int rc = isaac_reset_envs(c, &g, st, mask, d);
     free(mask);
     if (rc) return rc;
@@ -1076,6 +1076,10 @@ int or_reset_all(const or_cfg* c, or_state* st, const or_draws* d, float* obs) {
     }
     free(scratch);
     return 0;
+}
+
+int or_reset_all(const or_cfg* c, or_state* st, const or_draws* d, float* obs) {
+    return or_reset_idx(c, st, NULL, d, obs);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1242,3 +1246,134 @@ int or_step(const or_cfg* c, or_state* st, const float* act_cont, const int32_t*
         return step_standalone(c, &g, st, act_cont, act_disc, override_wheels, d, obs, reward, trunc);
     return step_isaac(c, &g, st, act_cont, act_disc, d, obs, reward, trunc);
 }
+
+/* ---------------------------------------------------------------------------
+ *  Draws of the production (Philox) HIP kernel, restated on the host.
+ *
+ *  The reference draws torch.rand / torch.randint from a Mersenne stream
+ *  (ES:420, BM:302-305 / 386-389, DG:1223-1260, MC:252-258); the GPU kernel
+ *  draws the same quantities from Philox4x32-10 keyed by the global env id
+ *  (swarm_step_impl.h philox4x32 / rng4 / ChunkRng / u01_of5 / u01_of7 /
+ *  draw_turn / spawn_isaac / spawn_mc). This function regenerates exactly those
+ *  values for one tick, laid out like the replayed reference draws, so the
+ *  oracle can check the production kernel element by element: only the source
+ *  of the uniforms differs from the reference-pinned replay path.
+ * ------------------------------------------------------------------------- */
+static void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        const uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+        c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+/* rng4(L, robot, block, purpose, tick): counter (genv, robot | block << 8 | purpose << 24, tick lo, tick hi) */
+static void rng4_host(uint64_t seed, uint32_t genv, uint32_t robot, uint32_t block, uint32_t purpose, uint64_t tick,
+                      uint32_t out[4]) {
+    out[0] = genv;
+    out[1] = robot | (block << 8) | (purpose << 24);
+    out[2] = (uint32_t)tick;
+    out[3] = (uint32_t)(tick >> 32);
+    philox4x32_10(out, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+static float u24(uint32_t v) { return (float)(v >> 8) * (1.0f / 16777216.0f); }
+
+static float u_of5(const uint32_t r[4], int w) {
+    uint32_t v;
+    switch (w) {
+    case 0: v = r[0] >> 8; break;
+    case 1: v = r[1] >> 8; break;
+    case 2: v = r[2] >> 8; break;
+    case 3: v = r[3] >> 8; break;
+    default: v = (r[0] & 0xFFu) | ((r[1] & 0xFFu) << 8) | ((r[2] & 0xFFu) << 16); break;
+    }
+    return (float)v * (1.0f / 16777216.0f);
+}
+
+static float u_of7(const uint32_t r[4], int w) {
+    const uint64_t lo = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+    const uint64_t hi = (uint64_t)r[2] | ((uint64_t)r[3] << 32);
+    const int o = 18 * w;
+    uint64_t v;
+    if (o + 18 <= 64) v = lo >> o;
+    else if (o >= 64) v = hi >> (o - 64);
+    else v = (lo >> o) | (hi << (64 - o));
+    return (float)(uint32_t)(v & 0x3FFFFull) * (1.0f / 262144.0f);
+}
+
+/* Packet-loss uniforms (E,N,N) of one purpose: robot i's neighbour j is in part
+ * p = j / C (C = ceil(N / parts)); parts = 3 for the step kernel's layout 103,
+ * 1 for the reset kernel and layout 1, 4 for layout 4. Entries j == i unused. */
+static void philox_rab(uint64_t seed, int64_t env_offset, int E, int N, int parts, uint32_t purpose, uint64_t tick,
+                       float* out) {
+    const int C = (N + parts - 1) / parts;
+    const int k18 = (C == 6 || C == 7);
+    for (int e = 0; e < E; e++) {
+        const uint32_t genv = (uint32_t)((uint64_t)env_offset + (uint64_t)e);
+        for (int i = 0; i < N; i++) {
+            float* row = out + ((size_t)e * N + i) * N;
+            for (int p = 0; p < parts; p++) {
+                const int j0 = p * C, j1 = j0 + C < N ? j0 + C : N;
+                uint32_t rb[4] = {0, 0, 0, 0};
+                for (int j = j0; j < j1; j++) {
+                    const int jj = j - j0;
+                    if (k18) {
+                        if (jj == 0) rng4_host(seed, genv, (uint32_t)i, (uint32_t)(16 * p), purpose, tick, rb);
+                        row[j] = u_of7(rb, jj);
+                    } else {
+                        if (jj % 5 == 0)
+                            rng4_host(seed, genv, (uint32_t)i, (uint32_t)(16 * p + jj / 5), purpose, tick, rb);
+                        row[j] = u_of5(rb, jj % 5);
+                    }
+                }
+            }
+        }
+    }
+}
+
+int or_philox_draws(uint64_t seed, int64_t env_offset, int E, int N, int parts, uint64_t tick, int profile,
+                    int spawn_k, float* rab_obs, float* rab_dispatch, int32_t* turns, float* spawn_u,
+                    float* spawn_yaw_u) {
+    enum { P_RAB_OBS = 1, P_RAB_DISPATCH = 2, P_TURN = 3, P_SPAWN = 8, P_SPAWN_YAW = 9 };
+    if (E < 1 || N < 1 || N > 64 || parts < 1) return -1;
+    if (rab_obs) philox_rab(seed, env_offset, E, N, parts, P_RAB_OBS, tick, rab_obs);
+    if (rab_dispatch) philox_rab(seed, env_offset, E, N, parts, P_RAB_DISPATCH, tick, rab_dispatch);
+    for (int e = 0; e < E; e++) {
+        const uint32_t genv = (uint32_t)((uint64_t)env_offset + (uint64_t)e);
+        for (int i = 0; i < N; i++) {
+            const size_t q = (size_t)e * N + i, EN = (size_t)E * N;
+            uint32_t r[4] = {0, 0, 0, 0};
+            if (turns)
+                for (int slot = 0; slot < 3; slot++) {
+                    rng4_host(seed, genv, (uint32_t)i, 0u, P_TURN + (uint32_t)slot, tick, r);
+                    turns[slot * EN + q] = 1 + (int32_t)(r[0] & 3u);
+                }
+            if (spawn_u && profile == OR_ISAAC) {
+                for (int k = 0; k < spawn_k; k++) {
+                    if ((k & 1) == 0) rng4_host(seed, genv, (uint32_t)i, (uint32_t)(k >> 1), P_SPAWN, tick, r);
+                    spawn_u[((size_t)k * EN + q) * 2 + 0] = u24((k & 1) ? r[2] : r[0]);
+                    spawn_u[((size_t)k * EN + q) * 2 + 1] = u24((k & 1) ? r[3] : r[1]);
+                }
+            } else if (spawn_u) {
+                rng4_host(seed, genv, (uint32_t)i, 0u, P_SPAWN, tick, r);
+                spawn_u[q] = u24(r[0]);
+                spawn_u[EN + q] = u24(r[1]);
+                spawn_u[2 * EN + q] = u24(r[2]);
+            }
+            if (spawn_yaw_u && profile == OR_ISAAC) {
+                rng4_host(seed, genv, (uint32_t)i, 0u, P_SPAWN_YAW, tick, r);
+                spawn_yaw_u[q] = u24(r[0]);
+            }
+        }
+    }
+    return 0;
+}
+
+/* test hook: one Philox4x32-10 block (known-answer checks) */
+void or_philox4x32(uint32_t* ctr, uint32_t k0, uint32_t k1) { philox4x32_10(ctr, k0, k1); }

@@ -75,6 +75,10 @@ int or_step(const or_cfg* cfg, or_state* st,
 /* DirectMARLEnv.reset(): _reset_idx(all) then observations (isaac profile). */
 int or_reset_all(const or_cfg* cfg, or_state* st, const or_draws* draws, float* obs_out);
 
+/* DirectMARLEnv._reset_idx(env_ids) (isaac profile, DG:1242-1273) for the envs whose
+ * mask byte is non-zero, then observations of all envs (NULL mask = all envs). */
+int or_reset_idx(const or_cfg* cfg, or_state* st, const uint8_t* env_mask, const or_draws* draws, float* obs_out);
+
 /* Sensor bundle of the current state (cache + observation), no stepping. */
 int or_observe(const or_cfg* cfg, or_state* st, const float* rab_u, float* obs_out);
 
@@ -86,6 +90,17 @@ void or_critic_state(const or_cfg* cfg, const float* pos, const float* yaw, floa
 
 /* Nudge every cos/sin/atan2/exp result by `ulps` ulp (0 = off): conditioning probe for tests. */
 void or_set_libm_perturb(int ulps);
+
+/* The production HIP kernel's Philox draws for one tick, laid out like or_draws
+ * (rab (E,N,N); turns (3,E,N); isaac spawn (spawn_k,E,N,2) + yaw (E,N);
+ * standalone spawn (3,E,N)). parts: neighbour parts of the kernel layout (3 =
+ * layout 103, 1 = reset kernel / layout 1). Any output may be NULL. */
+int or_philox_draws(uint64_t seed, int64_t env_offset, int E, int N, int parts, uint64_t tick, int profile,
+                    int spawn_k, float* rab_obs, float* rab_dispatch, int32_t* turns, float* spawn_u,
+                    float* spawn_yaw_u);
+
+/* One Philox4x32-10 block in place (test hook for known-answer vectors). */
+void or_philox4x32(uint32_t* ctr, uint32_t k0, uint32_t k1);
 
 /* Seed the oracle's private generator (MT19937, torch-compatible stream). */
 void or_seed(uint64_t seed);

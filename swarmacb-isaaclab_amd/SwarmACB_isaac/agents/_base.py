@@ -72,6 +72,22 @@ class RolloutStorage:
         yield from R.windowed(spec, arrays, order, starts, per_batch, R.row_bytes(spec, arrays, L, 0), mode=0,
                               chunks=chunks, n_items=n, L=L, T=T, E=E, N=N)
 
+    def sequence_batch_count(self, sequence_length: int, mini_batch_size: int) -> int:
+        """Number of minibatches _sequence_batches yields (multi-GPU ranks agree on a count)."""
+        T = self.ptr
+        if T <= 0:
+            return 0
+        L = max(1, min(int(sequence_length), T))
+        _chunks, n = R.sequence_chunks(self.dones[:T], self.num_agents, L)
+        return len(R.batch_starts(n, max(1, int(mini_batch_size) // L)))
+
+    def flat_batch_count(self, mini_batch_size: int) -> int:
+        """Number of minibatches _flat_batches yields."""
+        total = self.ptr * self.num_envs * self.num_agents
+        mb = int(mini_batch_size)
+        usable = total if total < mb else total - total % mb
+        return len(range(0, usable, mb))
+
     def _flat_batches(self, spec, mini_batch_size: int):
         """Focal-agent minibatches over all T*E*N agent rows (poca_buffer.py:202-238)."""
         T, E, N = self.ptr, self.num_envs, self.num_agents

@@ -2,7 +2,8 @@
 
 * `poca_checkpoint` / `save_poca_checkpoint` write the dict of
   PT:1056-1083 (`POCATrainer.save_checkpoint`), key for key, so a checkpoint
-  written here loads in the reference's `play.py` and trainer and vice versa.
+  written here loads in the reference's `play.py` (and, when it carries the
+  optimizer state, resumes in its trainer) and vice versa.
 * `load_poca_checkpoint` follows PT:1085-1106: the paper-parity version must
   match and the actor / critic (/ optimizer) state dicts must load strictly.
   Files are read with `torch.load(weights_only=True)`: a checkpoint holds
@@ -35,8 +36,17 @@ def poca_checkpoint(actor, critic: POCACritic, optimizer=None, *, obs_dim: int, 
                     sequence_length: int = 0, critic_hidden_dim: int = 256, critic_num_layers: int = 2,
                     critic_num_heads: int = 4, decision_period: int = 5, state_dim: int = 5,
                     act_dim: int | None = None) -> dict:
-    """The checkpoint dict of PT:1057-1083 for these modules."""
+    """The checkpoint dict of PT:1057-1083 for these modules. A checkpoint without an
+    optimizer state loads in play.py only: the reference's load_checkpoint
+    (PT:1085-1106) hands the empty dict to ``optimizer.load_state_dict``."""
     recurrent = isinstance(actor, RecurrentDiscreteActor)
+    if recurrent:
+        # ML-Agents total memory (h and c) = 2 x LSTM units (poca_networks.py:85-113)
+        total = 2 * int(actor.hidden_size)
+        if memory_size in (0, None):
+            memory_size = total
+        elif int(memory_size) != total:
+            raise ValueError(f"memory_size {memory_size} disagrees with the recurrent actor's {total}")
     discrete = isinstance(actor, (DiscreteActor, RecurrentDiscreteActor))
     return {
         "paper_parity_version": PAPER_PARITY_VERSION,

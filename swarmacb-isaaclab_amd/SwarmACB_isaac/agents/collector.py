@@ -206,7 +206,8 @@ class POCARolloutCollector:
             # the terminal-state value is multiplied by the time-out flags (PT:575-583): when the
             # host mirror says no env timed out in this decision it is 0 for every env, and the
             # critic pass is skipped (critic_pass with memory does not advance the memory)
-            if self.env.engine.last_timeouts:
+            engine = getattr(self.env, "engine", None)
+            if engine is None or engine.last_timeouts:
                 terminal = self.env.completed_terminal_critic_state
                 if self.recurrent:
                     tv = self.critic.critic_pass(terminal, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)

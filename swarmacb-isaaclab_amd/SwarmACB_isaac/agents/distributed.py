@@ -1,0 +1,134 @@
+"""Training collectives of the multi-GPU trainers.
+
+The reference trains on one GPU (its scale-out is SLURM seed arrays,
+scripts/hpc/run_training_common.sh). Here the arenas are sharded over one
+process per GPU (env physics needs no exchange, shard.py) and the trainers keep
+ONE global update, as if every arena sat on one device:
+
+* advantage normalisation over the experiences of all ranks
+  (poca_trainer.py:800-805, option_critic_trainer.py:674-678,
+  learned_option_critic_trainer.py:1423-1426): a 2-float all-reduce for the
+  mean, then a 1-float all-reduce of the squared deviations (two-pass, the
+  same arithmetic as ``std(unbiased=False)``);
+* the ML-Agents ``buffer_size`` trigger on the global experience count
+  (poca_trainer.py:900-908) and the episode clock on the global max length
+  (poca_trainer.py:890);
+* per optimizer step, the loss of each rank is its share of the GLOBAL
+  minibatch mean (sum of its terms / the global term count), and ONE
+  all-reduce (sum) of the flattened gradients of all parameters makes every
+  rank's gradient the gradient of the global minibatch loss. The gradients
+  live in one persistent flat fp32 buffer (each ``param.grad`` is a view of
+  it), so the exchange is a single RCCL call over xGMI with no packing copies:
+  0.74 MB for cyclamen POCA, 2.2 MB for OC2 — one ring all-reduce at
+  2·(7/8)·S / 153 GB/s per link ≈ 8-25 µs on 8 MI355X.
+
+With one process (``torch.distributed`` not initialised) every method is the
+identity and the trainers run the reference's arithmetic unchanged.
+"""
+
+from __future__ import annotations
+
+import torch
+
+
+class TrainerComm:
+    """The collectives of one trainer process (backend "nccl" = RCCL on ROCm, or "gloo")."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.group = group
+        self.dist = dist if dist.is_available() and dist.is_initialized() else None
+        self.world = self.dist.get_world_size(group) if self.dist is not None else 1
+        self.rank = self.dist.get_rank(group) if self.dist is not None else 0
+        self.backend = self.dist.get_backend(group) if self.dist is not None else None
+        self.flat_grad: torch.Tensor | None = None
+        self._params: list[torch.nn.Parameter] = []
+
+    @property
+    def active(self) -> bool:
+        return self.world > 1
+
+    # ------------------------------------------------------------ scalars
+    def _reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if not self.active:
+            return t
+        dev = t.device
+        x = t.cpu() if (self.backend == "gloo" and dev.type != "cpu") else t
+        ops = {"sum": self.dist.ReduceOp.SUM, "max": self.dist.ReduceOp.MAX, "min": self.dist.ReduceOp.MIN}
+        self.dist.all_reduce(x, op=ops[op], group=self.group)
+        if x is not t:
+            t.copy_(x)
+        return t
+
+    def sum_int(self, v: int) -> int:
+        return int(self._reduce(torch.tensor([int(v)], dtype=torch.int64, device=self._dev()))[0]) \
+            if self.active else int(v)
+
+    def max_int(self, v: int) -> int:
+        return int(self._reduce(torch.tensor([int(v)], dtype=torch.int64, device=self._dev()), "max")[0]) \
+            if self.active else int(v)
+
+    def min_int(self, v: int) -> int:
+        return int(self._reduce(torch.tensor([int(v)], dtype=torch.int64, device=self._dev()), "min")[0]) \
+            if self.active else int(v)
+
+    def sum_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        """All-reduced copy of t (sum over ranks)."""
+        return self._reduce(t.clone()) if self.active else t
+
+    def _dev(self):
+        if self.backend == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    # ------------------------------------------------------------ advantages
+    def normalize_(self, adv: torch.Tensor, eps: float = 1e-10) -> torch.Tensor:
+        """adv <- (adv - mean) / (std + eps) over the elements of all ranks, in place."""
+        if not self.active:
+            mean = adv.mean()
+            std = adv.std(unbiased=False)
+            adv.copy_((adv - mean) / (std + eps))
+            return adv
+        s = torch.stack([adv.double().sum(), torch.tensor(float(adv.numel()), dtype=torch.float64,
+                                                          device=adv.device)])
+        s = self._reduce(s)
+        mean = s[0] / s[1]
+        sq = self._reduce((adv.double() - mean).square().sum().reshape(1))[0]
+        std = torch.sqrt(sq / s[1])
+        adv.copy_(((adv - mean.float()) / (std.float() + eps)))
+        return adv
+
+    # ------------------------------------------------------------ gradients
+    def bind_flat_grads(self, params) -> torch.Tensor | None:
+        """Back every parameter's .grad by a view of one flat fp32 buffer (multi-rank only)."""
+        self._params = [p for p in params if p.requires_grad]
+        if not self.active or not self._params:
+            return None
+        dev = self._params[0].device
+        n = sum(p.numel() for p in self._params)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self._params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        return self.flat_grad
+
+    def zero_grad(self, optimizer):
+        if self.flat_grad is not None:
+            self.flat_grad.zero_()
+        else:
+            optimizer.zero_grad()
+
+    def all_reduce_grads(self):
+        """Sum of every rank's gradient (each rank's loss is already its share of the global mean)."""
+        if self.flat_grad is None:
+            return
+        for p in self._params:   # a parameter autograd did not reach must keep its view
+            if p.grad is None or p.grad.data_ptr() < self.flat_grad.data_ptr():
+                raise RuntimeError("a parameter's .grad was re-bound away from the flat gradient buffer")
+        self._reduce(self.flat_grad)
+
+    def global_count(self, local: torch.Tensor) -> torch.Tensor:
+        """Sum over ranks of a (device, float) term count (for the loss denominators)."""
+        return self._reduce(local.detach().clone()) if self.active else local

@@ -193,12 +193,14 @@ int32_t swarm_reset(swarm_handle_t* h, const swarm_state_t* state, const uint8_t
     // host mirror: per-env view only needed when a partial mask is used
     if (env_mask_host) {
         if (!h->lens_exact) {
-            // reconstruct per-env lengths: without a full view we conservatively
-            // assume the non-masked envs share the mirror's most common value
-            int64_t best = 0, cnt = -1;
-            for (auto& kv : h->mirror.buckets)
-                if (kv.second > cnt) { cnt = kv.second; best = kv.first + h->mirror.offset; }
-            h->lens.assign(E, (int32_t)best);
+            // the histogram no longer says which env holds which length: read the
+            // device's episode_length_buf (one copy + sync, only on this host-mask
+            // path, which already ships a host mask to the device)
+            h->lens.resize(E);
+            if (hipMemcpyAsync(h->lens.data(), state->episode_length, (size_t)E * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return hip_status();
         }
         for (int e = 0; e < E; ++e)
             if (env_mask_host[e]) h->lens[e] = 0;

@@ -84,11 +84,19 @@ def test_playback_refusals():
         CK.actor_from_checkpoint(dict(ckpt, trainer_type="learned_option_critic"), obs)
 
 
+def test_recurrent_memory_size_is_validated():
+    actor, critic, obs = _modules("cyclamen")
+    with pytest.raises(ValueError):
+        CK.poca_checkpoint(actor, critic, obs_dim=obs, memory_size=64)
+
+
 def test_legacy_memory_size_semantics():
     """Checkpoints older than the parity revision stored the LSTM unit count
     (poca_networks.py:116-127): playback doubles it."""
     actor, critic, obs = _modules("cyclamen")
-    ckpt = CK.poca_checkpoint(actor, critic, obs_dim=obs, hidden_dim=128, num_layers=1, memory_size=64)
+    ckpt = CK.poca_checkpoint(actor, critic, obs_dim=obs, hidden_dim=128, num_layers=1)
+    assert ckpt["memory_size"] == 128          # derived from the actor (ML-Agents total)
+    ckpt["memory_size"] = 64                   # a pre-parity checkpoint stored the unit count
     del ckpt["memory_size_semantics"]
     rebuilt, info = CK.actor_from_checkpoint(ckpt, obs)
     assert info["memory_size"] == 128 and rebuilt.hidden_size == 64

@@ -75,7 +75,7 @@ def _gpu_step(eng, fx, t, meta, device):
 def test_gpu_matches_reference_golden(name, layout, gpu_device):
     fx = parity.load(name)
     eng, _, meta = _engine(fx, gpu_device, layout=layout)
-    failures = []
+    failures, stats = [], {}
     for t in range(fx["obs"].shape[0]):
         got = _gpu_step(eng, fx, t, meta, gpu_device)
         base, spread = parity.envelope(fx, t)
@@ -83,9 +83,10 @@ def test_gpu_matches_reference_golden(name, layout, gpu_device):
         if meta["profile"] == "isaac" and not meta["discrete"]:
             ref.pop("wheel_l", None)  # continuous variants do not read the wheel cache
             ref.pop("wheel_r", None)
-        failures += [f"step {t} vs reference: {e}" for e in parity.compare(got, ref, spread)]
+        failures += [f"step {t} vs reference: {e}" for e in parity.compare(got, ref, spread, stats=stats)]
         failures += [f"step {t} vs oracle: {e}" for e in parity.compare(got, base, spread, keys=list(ref))]
     eng.close()
+    parity.record_stats(f"gpu_vs_reference/{name}/layout{layout}", stats)
     assert not failures, "\n".join(failures[:12])
 
 
@@ -185,15 +186,11 @@ def test_gpu_random_states_vs_oracle(mission, profile, discrete, layout, gpu_dev
         o2 = O.OracleEnv(mission, profile, E, N, obs_dim, discrete, max_len)
         o2.s.update({k: np.copy(v) for k, v in s.items()})
         ob2, rw2, tr2 = parity.perturbed_step(o2, p, actions=acts, override=ovr, draws=draws)
-        out2 = dict(o2.s, obs=ob2, reward=rw2, trunc=tr2)
-        for k, v in out2.items():
-            if k not in ref:
-                continue
-            if k in parity.FLOAT_KEYS:
-                spread[k] = np.maximum(spread.get(k, 0.0), np.abs(v.astype(np.float64) - ref[k].astype(np.float64)))
-            else:
-                spread[k] = spread.get(k, np.zeros(np.shape(v), bool)) | (np.asarray(v) != np.asarray(ref[k]))
-    errs = parity.compare(got, ref, spread)
+        parity.accumulate_spread(spread, dict(o2.s, obs=ob2, reward=rw2, trunc=tr2), ref)
+    stats = {}
+    errs = parity.compare(got, ref, spread, stats=stats)
+    parity.record_stats(f"gpu_random_states/{mission}/{profile}/{'disc' if discrete else 'cont'}/layout{layout}",
+                        stats)
     eng.close()
     assert not errs, "\n".join(errs[:12])
 

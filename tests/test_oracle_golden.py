@@ -18,11 +18,12 @@ from oracle import oracle as O
 def test_oracle_matches_reference(name):
     fx = parity.load(name)
     T = fx["obs"].shape[0]
-    failures = []
+    failures, stats = [], {}
     for t in range(T):
         base, spread = parity.envelope(fx, t)
-        errs = parity.compare(base, parity.reference_after(fx, t), spread)
+        errs = parity.compare(base, parity.reference_after(fx, t), spread, stats=stats)
         failures += [f"step {t}: {e}" for e in errs]
+    parity.record_stats(f"oracle_vs_reference/{name}", stats)
     assert not failures, "\n".join(failures[:10])
 
 
