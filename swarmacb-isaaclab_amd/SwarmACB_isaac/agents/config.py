@@ -321,3 +321,91 @@ def make_env_cfg(task_id: str, variant: str, env_overrides: Mapping[str, Any], t
     for key in ignored:
         print(f"[Train] Warning: ignored unknown environment override {key!r}")
     return env_cfg
+
+
+_TRAINER_LABELS = {"learned_option_critic": "Learned Option-Critic (Phase 2)",
+                   "option_critic": "Fixed Option-Critic (Phase 1)", "poca": "POCA"}
+
+
+def config_summary(run_name: str, variant: str, cfg: Any, env_ov: Mapping[str, Any]) -> list[tuple[str, str]]:
+    """(section, "label : value") rows of the console summary (config_loader.py:193-322)."""
+    rows: list[tuple[str, str]] = []
+    tt = getattr(cfg, "trainer_type", "poca")
+
+    def add(sec, label, value):
+        rows.append((sec, f"{label:20s}: {value}"))
+
+    add("Run", "Run name", run_name)
+    add("Run", "CASA variant", variant)
+    add("Run", "Trainer", _TRAINER_LABELS.get(tt, tt))
+    h = "Hyperparameters"
+    add(h, "batch_size", cfg.mini_batch_size)
+    add(h, "learning_rate", f"{cfg.lr}  (schedule: {cfg.lr_schedule})")
+    add(h, "beta", f"{cfg.beta}  (schedule: {cfg.beta_schedule})")
+    add(h, "epsilon", f"{cfg.clip_eps}  (schedule: {cfg.eps_schedule})")
+    for label, attr in (("lambd", "lam"), ("num_epoch", "num_epochs"), ("gamma", "gamma"),
+                        ("termination_penalty", "termination_penalty"), ("termination_coef", "termination_coef"),
+                        ("termination_entropy", "termination_entropy_coef"), ("value_coef", "value_coef"),
+                        ("option_value_coef", "option_value_coef"), ("baseline_coef", "baseline_coef"),
+                        ("intra_option_coef", "intra_option_coef"), ("selector_coef", "selector_coef"),
+                        ("local_option_value", "local_option_value_coef"),
+                        ("action_baseline", "action_baseline_coef"), ("option_baseline", "option_baseline_coef"),
+                        ("option_entropy", "option_entropy_coef"),
+                        ("attention_diversity", "attention_diversity_coef"),
+                        ("attention_temporal", "attention_temporal_coef"),
+                        ("initial_termination", "initial_termination_probability"),
+                        ("actor_learning_rate", "actor_lr"), ("actor_max_grad_norm", "actor_max_grad_norm"),
+                        ("target_kl", "target_kl"), ("adaptive_actor_lr", "adaptive_actor_lr"),
+                        ("fused_optimizer", "fused_optimizer"), ("matmul_precision", "matmul_precision")):
+        if hasattr(cfg, attr):
+            add(h, label, getattr(cfg, attr))
+    if hasattr(cfg, "option_balance_coef"):
+        add(h, "option_balance", f"{cfg.option_balance_coef} -> {cfg.option_balance_final_coef}")
+        add(h, "option_exploration", f"epsilon={cfg.option_epsilon_start} -> {cfg.option_epsilon_final} "
+                                     f"({cfg.option_epsilon_schedule}, first "
+                                     f"{100.0 * cfg.option_epsilon_decay_fraction:g}% of training)")
+    n = "Network"
+    add(n, "hidden_units", cfg.hidden_dim)
+    add(n, "num_layers", cfg.num_layers)
+    add(n, "critic_hidden", cfg.critic_hidden_dim)
+    add(n, "critic_layers", cfg.critic_num_layers)
+    add(n, "critic_heads", cfg.critic_num_heads)
+    if hasattr(cfg, "option_hidden_dim"):
+        add(n, "option_hidden", cfg.option_hidden_dim)
+        add(n, "option_layers", cfg.option_num_layers)
+    if hasattr(cfg, "num_options"):
+        add(n, "learned_options" if tt == "learned_option_critic" else "fixed_options", cfg.num_options)
+    if cfg.recurrent:
+        add(n, "memory_size", f"{cfg.memory_size} ({cfg.memory_size // 2} LSTM units)")
+        if hasattr(cfg, "option_memory_size"):
+            add(n, "option_memory", f"{cfg.option_memory_size} ({cfg.option_memory_size // 2} LSTM units/option)")
+        add(n, "sequence_length", cfg.sequence_length)
+    t = "Training"
+    add(t, "seed", cfg.seed)
+    add(t, "max_steps", f"{cfg.total_timesteps:,}")
+    if cfg.buffer_size_hint:
+        add(t, "buffer_size", f"{cfg.buffer_size_hint:,} (ML-Agents reference target)")
+    add(t, "time_horizon", cfg.horizon)
+    add(t, "decision_period", cfg.decision_period)
+    add(t, "checkpoint_interval", f"{cfg.checkpoint_interval:,}")
+    add(t, "summary_freq", f"{cfg.summary_freq:,}")
+    if cfg.reward_strength != 1.0:
+        add(t, "reward_strength", cfg.reward_strength)
+    for k, v in env_ov.items():
+        add("Environment overrides", k, v)
+    return rows
+
+
+def print_config(run_name: str, variant: str, cfg: Any, env_ov: Mapping[str, Any]) -> None:
+    """Console summary of a resolved config (config_loader.py:193-322)."""
+    sep = "-" * 60
+    print(f"\n{sep}\n  SwarmACB Training Config\n{sep}")
+    section = None
+    for sec, line in config_summary(run_name, variant, cfg, env_ov):
+        if sec != section and sec != "Run":
+            if section == "Run":
+                print(sep)
+            print(f"  {sec}")
+        section = sec
+        print(f"    {line}" if sec != "Run" else f"  {line}")
+    print(f"{sep}\n")
