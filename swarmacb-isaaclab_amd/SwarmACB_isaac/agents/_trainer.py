@@ -1,0 +1,277 @@
+"""Machinery the three trainers share (POCA, fixed-option OC, learned-option OC2).
+
+The reference repeats it per trainer (poca_trainer.py:425-435 / 858-1050 /
+1109-1123, option_critic_trainer.py:243-252 / 759-888 / 947-959,
+learned_option_critic_trainer.py's equivalents): ML-Agents linear schedules,
+the ``buffer_size`` update trigger over complete decisions, the train loop with
+its progress bar, summaries and checkpoint rotation. Here it is written once,
+on top of the multi-GPU collectives of agents/distributed.py.
+"""
+
+from __future__ import annotations
+
+import itertools
+import time
+from pathlib import Path
+
+import torch
+
+from .distributed import TrainerComm
+from .metrics import make_writer
+
+
+class PolynomialDecay:
+    """ML-Agents ModelUtils.polynomial_decay (poca_trainer.py:117-137): from `initial`
+    to `min_value` over `max_step` agent-decisions."""
+
+    def __init__(self, initial: float, min_value: float, max_step: int, power: float = 1.0):
+        self.initial, self.min_value, self.max_step, self.power = initial, min_value, max(max_step, 1), power
+
+    def get(self, step: int) -> float:
+        step = min(step, self.max_step)
+        return (self.initial - self.min_value) * (1.0 - step / self.max_step) ** self.power + self.min_value
+
+
+def masked_mean(loss, mask, denom=None):
+    """Mean over the active terms: the reference's form (PT:159-162, 185-190) unless a
+    global denominator (multi-GPU) is given."""
+    if mask is not None:
+        active = mask.to(dtype=loss.dtype)
+        while active.ndim < loss.ndim:
+            active = active.unsqueeze(-1)
+        active = active.expand_as(loss)
+        num = (loss * active).sum()
+        return num / (denom if denom is not None else active.sum().clamp_min(1.0))
+    return loss.sum() / denom if denom is not None else loss.mean()
+
+
+def trust_region_value_loss(values, old_values, returns, epsilon: float, mask=None, denom=None):
+    """ML-Agents trust_region_value_loss (poca_trainer.py:144-162)."""
+    clipped = old_values + (values - old_values).clamp(-epsilon, epsilon)
+    loss = torch.max((returns - values) ** 2, (returns - clipped) ** 2)
+    return masked_mean(loss, mask, denom)
+
+
+def trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilon: float, mask=None, denom=None):
+    """ML-Agents trust_region_policy_loss, ratio clipped per action dimension
+    (poca_trainer.py:165-191)."""
+    r_theta = (log_probs - old_log_probs).exp()
+    loss = -torch.min(r_theta * advantages, r_theta.clamp(1.0 - epsilon, 1.0 + epsilon) * advantages)
+    return masked_mean(loss, mask, denom)
+
+
+def stack_obs(obs, agents) -> torch.Tensor:
+    """The (E, N, D) observation of an obs dict (PT:470-474)."""
+    x = torch.stack([obs[a] for a in agents], dim=1) if isinstance(obs, dict) else obs
+    if x.ndim == 5:                                   # grid observations
+        x = x.reshape(x.shape[0], x.shape[1], -1)
+    return x.contiguous()
+
+
+class TrainerBase:
+    """Schedules, update trigger, train loop, checkpoint rotation."""
+
+    algo = "Trainer"            # console / progress-bar name
+    ckpt_prefix = "trainer"     # <prefix>_<step>.pt, <prefix>_final.pt
+
+    def _init_common(self, env, cfg, group, writer):
+        self.env = env
+        self.cfg = cfg
+        self.unwrapped = env.unwrapped
+        self.device = torch.device(self.unwrapped.device)
+        self.comm = TrainerComm(group)
+        self.num_envs = self.unwrapped.scene.num_envs
+        cfg_env = self.unwrapped.cfg
+        self.num_agents = getattr(cfg_env, "num_agents", getattr(cfg_env, "num_robots", None))
+        self.discrete = bool(getattr(cfg_env, "discrete_actions", False))
+        self.variant = getattr(cfg_env, "variant", None)
+        self.agents = list(cfg_env.possible_agents)
+        sample = self.env.reset()[0][self.agents[0]]
+        self.obs_dim = int(sample[0].numel()) if sample.ndim == 4 else int(sample.shape[1])
+        self.state_dim = 5
+        c = cfg
+        self.decision_period = int(c.decision_period)
+        self.lr_schedule = PolynomialDecay(c.lr, 1e-10, c.total_timesteps) if c.lr_schedule == "linear" else None
+        self.eps_schedule = (PolynomialDecay(c.clip_eps, 0.1, c.total_timesteps)
+                             if c.eps_schedule == "linear" else None)
+        self.beta_schedule = PolynomialDecay(c.beta, 1e-5, c.total_timesteps) if c.beta_schedule == "linear" else None
+        self.current_lr, self.current_eps, self.current_beta = c.lr, c.clip_eps, c.beta
+        self.reward_strength = c.reward_strength
+        self._next_checkpoint_step = c.checkpoint_interval
+        self._next_summary_step = c.summary_freq
+        self.global_step = 0
+        self.update_count = 0
+        self.writer = writer if writer is not None else make_writer(c.log_dir, self.comm.rank)
+        self.writer.add_text("hyperparameters", "\n".join(f"{k}: {v}" for k, v in vars(c).items()), 0)
+        self._completed_episode_returns: list[float] = []
+        self._completed_episode_lengths: list[float] = []
+        self._completed_group_rewards: list[float] = []
+        self._rollout_reward_history: list[float] = []
+        self._max_history = 100
+        # test / profiling hooks: called with (step index, params) after the gradient
+        # exchange and after the optimizer step
+        self.grad_hook = None
+        self.step_hook = None
+
+    def _buffer_capacity(self) -> int:
+        """horizon + the decisions the ML-Agents trigger may add, counted over ALL ranks
+        (poca_trainer.py:337-340, option_critic_trainer.py:207-210)."""
+        per_decision = self.num_envs * self.num_agents * self.comm.world
+        return self.cfg.horizon + (self.cfg.buffer_size_hint + per_decision - 1) // per_decision + 1
+
+    def _apply_schedules(self):
+        """poca_trainer.py:425-435."""
+        step = self.global_step
+        if self.lr_schedule is not None:
+            self.current_lr = self.lr_schedule.get(step)
+            for pg in self.optimizer.param_groups:
+                pg["lr"] = self.current_lr
+        if self.eps_schedule is not None:
+            self.current_eps = self.eps_schedule.get(step)
+        if self.beta_schedule is not None:
+            self.current_beta = self.beta_schedule.get(step)
+
+    def _drain_episodes(self):
+        r, ln, g = self.collector.recorder.drain()
+        self._completed_episode_returns += r
+        self._completed_episode_lengths += ln
+        self._completed_group_rewards += g
+
+    def _denominators(self, counts: list[torch.Tensor]):
+        """Global term counts of this minibatch (multi-GPU), else None (reference means)."""
+        if not self.comm.active:
+            return [None] * len(counts)
+        g = self.comm.global_count(torch.stack([c.to(torch.float32) for c in counts]))
+        return [x.clamp_min(1.0) for x in g.unbind(0)]
+
+    def _sequence_batches(self):
+        """One epoch of recurrent minibatches; multi-GPU ranks take mini_batch_size / world
+        rows each and stop together at the smallest local batch count."""
+        mb = max(1, self.cfg.mini_batch_size // self.comm.world)
+        it = self.buffer.get_sequence_batches(self.cfg.sequence_length, mb)
+        if self.comm.active:
+            it = itertools.islice(it, self.comm.min_int(
+                self.buffer.sequence_batch_count(self.cfg.sequence_length, mb)))
+        return it
+
+    def optimizer_step(self, loss: torch.Tensor, step_index: int):
+        self.comm.zero_grad(self.optimizer)
+        loss.backward()
+        self.comm.all_reduce_grads()
+        if self.grad_hook is not None:
+            self.grad_hook(step_index, self.params)
+        self.optimizer.step()
+        if self.step_hook is not None:
+            self.step_hook(step_index, self.params)
+
+    # ------------------------------------------------------------ train
+    def _rollout_until_trigger(self, obs_dict):
+        """Complete decisions until the global experience count exceeds buffer_size
+        (poca_trainer.py:882-908, option_critic_trainer.py:786-814)."""
+        c = self.cfg
+        self.buffer.reset()
+        per = self.num_envs * self.num_agents * self.comm.world
+        while self.global_step < c.total_timesteps:
+            remaining = c.total_timesteps - self.global_step
+            remaining_steps = max(1, (remaining + per - 1) // per)
+            episode_step = self.comm.max_int(int(self.unwrapped.episode_length_buf.max().item()))
+            episode_steps_left = max(1, (self.unwrapped.max_episode_length - episode_step + self.decision_period - 1)
+                                     // self.decision_period)
+            rollout_steps = min(c.horizon, remaining_steps, episode_steps_left)
+            obs_dict = self.collect_rollout(obs_dict, rollout_steps, reset_buffer=False)
+            if self.buffer.ptr * per > c.buffer_size_hint:
+                break
+        return obs_dict
+
+    def _on_train_start(self):
+        pass
+
+    def _postfix(self, metrics: dict, sps: float) -> dict:
+        return {"upd": self.update_count, "SPS": f"{sps:.0f}"}
+
+    def _log(self, metrics: dict, sps: float, mean_rollout_reward: float):
+        raise NotImplementedError
+
+    def _log_episodes(self, w, s):
+        """The completed-episode scalars every trainer writes (poca_trainer.py:1006-1033)."""
+        if self._completed_episode_returns:
+            ep = self._completed_episode_returns
+            w.add_scalar("Environment/Cumulative Reward", sum(ep) / len(ep), s)
+            ep.clear()
+        if self._completed_episode_lengths:
+            el = self._completed_episode_lengths
+            w.add_scalar("Environment/Episode Length", sum(el) / len(el), s)
+            el.clear()
+        if self._completed_group_rewards:
+            gr = self._completed_group_rewards
+            w.add_scalar("Extra/Group Reward Mean", sum(gr) / len(gr), s)
+            gr.clear()
+
+    def train(self):
+        """poca_trainer.py:858-1050 / option_critic_trainer.py:759-888."""
+        start_time = time.time()
+        obs_dict, _ = self.env.reset()
+        self._on_train_start()
+        ckpt_dir = Path(self.cfg.checkpoint_dir)
+        if self.comm.rank == 0:
+            ckpt_dir.mkdir(parents=True, exist_ok=True)
+        pbar = None
+        if self.comm.rank == 0:
+            from tqdm import tqdm
+
+            pbar = tqdm(total=self.cfg.total_timesteps, initial=self.global_step, desc=f"{self.algo} Training",
+                        unit="step", unit_scale=True, dynamic_ncols=True)
+        while self.global_step < self.cfg.total_timesteps:
+            prev_step = self.global_step
+            obs_dict = self._rollout_until_trigger(obs_dict)
+            metrics = self.update()
+            self._drain_episodes()
+            elapsed = time.time() - start_time
+            sps = self.global_step / elapsed if elapsed > 0 else 0.0
+            if pbar is not None:
+                pbar.update(min(self.global_step - prev_step, max(0, self.cfg.total_timesteps - pbar.n)))
+                pbar.set_postfix(**self._postfix(metrics, sps))
+            T = self.buffer.ptr
+            mean_rollout_reward = self.buffer.rewards[:T].sum(dim=0).mean().item()
+            self._rollout_reward_history.append(mean_rollout_reward)
+            if len(self._rollout_reward_history) > self._max_history:
+                self._rollout_reward_history.pop(0)
+            if self.global_step >= self._next_summary_step:
+                self._next_summary_step += self.cfg.summary_freq
+                self._log(metrics, sps, mean_rollout_reward)
+            if self.global_step >= self._next_checkpoint_step:
+                self.save_checkpoint(ckpt_dir / f"{self.ckpt_prefix}_{self.global_step}.pt")
+                self._next_checkpoint_step += self.cfg.checkpoint_interval
+                self._manage_checkpoints(ckpt_dir)
+        if pbar is not None:
+            pbar.close()
+        self.writer.close()
+        self.save_checkpoint(ckpt_dir / f"{self.ckpt_prefix}_final.pt")
+        elapsed = time.time() - start_time
+        if self.comm.rank == 0:
+            print(f"[{self.algo}] Done - {self.global_step:,} steps in {elapsed:.0f}s "
+                  f"({self.global_step / max(elapsed, 1e-9):.0f} SPS)")
+
+    # ------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, path):
+        """Rank 0 writes checkpoint_dict() (poca_trainer.py:1056-1083 and equivalents)."""
+        if self.comm.rank != 0:
+            return
+        torch.save(self.checkpoint_dict(), path)
+        print(f"[{self.algo}] Saved -> {path}")
+
+    def _rebind_grads(self):
+        if self.comm.flat_grad is not None:   # optimizer state loaded; keep grads bound to the flat buffer
+            self.comm.bind_flat_grads(self.params)
+
+    def _manage_checkpoints(self, ckpt_dir: Path):
+        """Keep the keep_checkpoints most recent numbered checkpoints (poca_trainer.py:1109-1123)."""
+        keep = self.cfg.keep_checkpoints
+        if keep <= 0 or self.comm.rank != 0:
+            return
+        numbered = sorted(ckpt_dir.glob(f"{self.ckpt_prefix}_*.pt"), key=lambda p: p.stat().st_mtime)
+        numbered = [p for p in numbered if p.stem != f"{self.ckpt_prefix}_final"]
+        while len(numbered) > keep:
+            old = numbered.pop(0)
+            old.unlink()
+            print(f"[{self.algo}] Removed old checkpoint -> {old.name}")
