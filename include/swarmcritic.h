@@ -31,16 +31,19 @@ typedef enum {
     SWARM_RSA_BASELINES = 1,  /* N sets per env (all_baselines): set i = [row i, rows N + j for j != i,
                                  increasing j]; R = 2N rows per env: 0..N-1 state-only embeddings,
                                  N..2N-1 state+action embeddings */
-    SWARM_RSA_SINGLE_OF_PAIRS = 2 /* one set per env from the BASELINES layout: entities = rows 0 .. N-1
+    SWARM_RSA_SINGLE_OF_PAIRS = 2, /* one set per env from the BASELINES layout: entities = rows 0 .. N-1
                                  of each env's 2N-row block, so the team value V(s) (critic_pass) and
                                  the baselines of one decision share one embedding / projection pass */
+    SWARM_RSA_ACTIONS_OF_PAIRS = 3 /* one set per env from the BASELINES layout: entities = rows N .. 2N-1
+                                 (the state+action rows), i.e. joint_action_pass's Q(s, a) — the
+                                 option-critic trainers' collective option value shares the pass too */
 } swarm_rsa_mode_t;
 
 /* pooled[(b * n_sets + s) * hidden + c] = mean over the N members of set s of
  *   LayerNorm( fc_out( softmax_k(q k^T / sqrt(hidden)) v ) + x )[c]   (per head; no affine, eps 1e-5)
  * x: [B][R][hidden] f32; qkv: [B][R][3*hidden] f32 (q | k | v); w_out: [hidden][hidden] (torch Linear
- * layout, out x in); b_out: [hidden]; n_sets = 1 (SINGLE, SINGLE_OF_PAIRS) or N (BASELINES);
- * R = N (SINGLE) or 2N (BASELINES, SINGLE_OF_PAIRS).
+ * layout, out x in); b_out: [hidden]; n_sets = 1 (SINGLE, *_OF_PAIRS) or N (BASELINES);
+ * R = N (SINGLE) or 2N (BASELINES, *_OF_PAIRS).
  * Supported: hidden = 128, heads in {1, 2, 4}, 1 <= N <= 20. fc_out runs on the matrix cores
  * (v_mfma_f32_16x16x4_f32: exact fp32 products). x, qkv and pooled must be 16-byte aligned. */
 int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,

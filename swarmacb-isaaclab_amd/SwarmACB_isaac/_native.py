@@ -69,7 +69,7 @@ class GatherField(C.Structure):
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
 CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
-RSA_SINGLE, RSA_BASELINES, RSA_SINGLE_OF_PAIRS = 0, 1, 2
+RSA_SINGLE, RSA_BASELINES, RSA_SINGLE_OF_PAIRS, RSA_ACTIONS_OF_PAIRS = 0, 1, 2, 3
 
 RECORD_MAX_MEMORIES = 12
 

@@ -8,10 +8,11 @@ from .config import (FixedOptionCriticConfig, LearnedOptionCriticConfig, POCACon
                      load_config, make_env_cfg)
 from .checkpoint import actor_from_checkpoint, evaluate, load_poca_checkpoint, poca_checkpoint, save_poca_checkpoint
 from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
+from .learned_option_critic_networks import LearnedOptionActor, SquashedNormal
 from .option_critic_buffer import FixedOptionRolloutBuffer
 from .option_critic_networks import FixedOptionManager
 from .poca_buffer import POCARolloutBuffer
 
 __all__ = ["DecisionRecorder", "POCARolloutCollector", "POCAConfig", "FixedOptionCriticConfig",
            "LearnedOptionCriticConfig", "apply_network_settings", "load_config", "make_env_cfg", "POCARolloutBuffer", "FixedOptionRolloutBuffer", "LearnedOptionRolloutBuffer",
-           "FixedOptionManager", "poca_checkpoint", "save_poca_checkpoint", "load_poca_checkpoint", "actor_from_checkpoint", "evaluate"]
+           "FixedOptionManager", "LearnedOptionActor", "SquashedNormal", "poca_checkpoint", "save_poca_checkpoint", "load_poca_checkpoint", "actor_from_checkpoint", "evaluate"]

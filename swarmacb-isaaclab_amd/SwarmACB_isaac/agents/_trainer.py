@@ -73,6 +73,7 @@ class TrainerBase:
 
     algo = "Trainer"            # console / progress-bar name
     ckpt_prefix = "trainer"     # <prefix>_<step>.pt, <prefix>_final.pt
+    sps_since_start = False     # SPS over this session's steps (OC2) or over global_step (POCA, OC)
 
     def _init_common(self, env, cfg, group, writer):
         self.env = env
@@ -186,6 +187,9 @@ class TrainerBase:
     def _on_train_start(self):
         pass
 
+    def _post_update(self, metrics: dict, update_seconds: float, step_delta: int):
+        pass
+
     def _postfix(self, metrics: dict, sps: float) -> dict:
         return {"upd": self.update_count, "SPS": f"{sps:.0f}"}
 
@@ -210,6 +214,7 @@ class TrainerBase:
     def train(self):
         """poca_trainer.py:858-1050 / option_critic_trainer.py:759-888."""
         start_time = time.time()
+        start_step = self.global_step if self.sps_since_start else 0
         obs_dict, _ = self.env.reset()
         self._on_train_start()
         ckpt_dir = Path(self.cfg.checkpoint_dir)
@@ -224,10 +229,12 @@ class TrainerBase:
         while self.global_step < self.cfg.total_timesteps:
             prev_step = self.global_step
             obs_dict = self._rollout_until_trigger(obs_dict)
+            t_update = time.perf_counter()
             metrics = self.update()
+            self._post_update(metrics, time.perf_counter() - t_update, self.global_step - prev_step)
             self._drain_episodes()
             elapsed = time.time() - start_time
-            sps = self.global_step / elapsed if elapsed > 0 else 0.0
+            sps = (self.global_step - start_step) / elapsed if elapsed > 0 else 0.0
             if pbar is not None:
                 pbar.update(min(self.global_step - prev_step, max(0, self.cfg.total_timesteps - pbar.n)))
                 pbar.set_postfix(**self._postfix(metrics, sps))

@@ -1,0 +1,812 @@
+"""Learned-option collective Option-Critic trainer, OC2 (drop-in for
+agents/learned_option_critic_trainer.py:LearnedOptionCriticTrainer, lines 170-2345).
+
+Same constructor ``LearnedOptionCriticTrainer(env, cfg)``, same
+``collect_rollout`` / ``update`` / ``train`` / ``save_checkpoint`` /
+``load_checkpoint`` surface and the same arithmetic: a shared recurrent
+Attention Option-Critic actor (epsilon-soft selection over attended option
+values, one continuous two-wheel Gaussian and one termination head per option),
+three centralised RSA critics (team V(s); counterfactual action baselines over
+(state, option) entities; collective option value Q(s, omega) and option
+baselines), PPO on the intra-option wheel policies against a frozen
+update-start copy of the actor with a KL early stop for the actor, the
+termination theorem at s', attention diversity / temporal regularisers,
+separate actor / critic Adam optimisers with gradient-norm clipping, the
+optional adaptive actor learning rate.
+
+What is MI355X-specific: the rollout is the fused decision loop
+(agents/option_collector.py: one step-kernel launch per decision, LSTM cells and
+the critic attention as HIP kernels, the option critic's two passes sharing one
+projection, one decision-record launch); the buffers' scan and gathers are HIP
+kernels; the update avoids the reference's per-minibatch host syncs except the
+one that decides the KL early stop; multi-GPU runs keep one global update (two
+flat gradient all-reduces per minibatch — actor 1.0 MB / critics 1.2 MB at the
+OC2 XOR config — plus the global KL that keeps every rank's early-stop
+decision identical; agents/distributed.py).
+"""
+
+from __future__ import annotations
+
+import copy
+import time
+
+import torch
+import torch.nn.functional as F
+import torch.optim as optim
+from torch.distributions import Bernoulli
+
+from ._trainer import PolynomialDecay, TrainerBase, stack_obs, trust_region_value_loss
+from .config import PAPER_PARITY_VERSION, LearnedOptionCriticConfig
+from .distributed import TrainerComm
+from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
+from .learned_option_critic_networks import (LEARNED_OPTION_CRITIC_VERSION, LearnedOptionActor,
+                                             termination_objective)
+from .option_collector import LearnedOptionCollector
+from .poca_networks import POCACritic
+
+__all__ = ["LearnedOptionCriticConfig", "LearnedOptionCriticTrainer", "stable_trust_region_policy_loss"]
+
+METRIC_NAMES = (
+    "intra_option_loss", "selector_loss", "local_option_value_loss", "local_option_value_mean",
+    "option_value_spread", "value_loss", "action_baseline_loss", "joint_option_value_loss", "option_baseline_loss",
+    "termination_loss", "action_entropy", "option_entropy", "option_balance_loss", "option_marginal_entropy",
+    "effective_options", "termination_entropy", "termination_prior_loss", "attention_diversity_loss",
+    "attention_temporal_loss", "mean_attention", "mean_beta", "mean_termination_advantage",
+    "mean_termination_signal", "termination_low_saturation", "termination_high_saturation", "action_approx_kl",
+    "option_approx_kl", "behavior_action_logp_error", "behavior_option_logp_error")
+OBJECTIVE_NAMES = (
+    "actor_objective", "critic_objective", "objective_intra_option", "objective_selector",
+    "objective_local_option_value", "objective_termination", "objective_termination_prior",
+    "objective_option_balance", "objective_attention_diversity", "objective_attention_temporal",
+    "objective_action_entropy", "objective_option_entropy", "objective_termination_entropy")
+_COLLECTOR_STATE = LearnedOptionCollector.MEMORIES + ("current_options",)
+
+
+def stable_trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilon: float, mask=None, denom=None):
+    """PPO policy loss with the log-ratio bounded to [-20, 20] before exp (LOT:45-72)."""
+    ratio = (log_probs - old_log_probs).clamp(-20.0, 20.0).exp()
+    loss = -torch.minimum(ratio * advantages, ratio.clamp(1.0 - epsilon, 1.0 + epsilon) * advantages)
+    if mask is None:
+        return loss.mean() if denom is None else loss.sum() / denom
+    active = mask.to(dtype=loss.dtype)
+    while active.ndim < loss.ndim:
+        active = active.unsqueeze(-1)
+    active = active.expand_as(loss)
+    return (loss * active).sum() / (denom if denom is not None else active.sum().clamp_min(1.0))
+
+
+class LearnedOptionCriticTrainer(TrainerBase):
+    """Train learned continuous options with collective counterfactual credit (LOT:170-2345)."""
+
+    algo = "LearnedOC"
+    ckpt_prefix = "option_critic_2"
+    sps_since_start = True
+    CHECKPOINT_VERSION = LEARNED_OPTION_CRITIC_VERSION
+    TRAINING_CHECKPOINT_VERSION = 6
+
+    def __init__(self, env, cfg: LearnedOptionCriticConfig | None = None, *, group=None, writer=None):
+        self._init_common(env, cfg or LearnedOptionCriticConfig(), group, writer)
+        cfg = self.cfg
+        if self.variant != "cyclamen":
+            raise ValueError("Learned Option-Critic Phase 2 starts from Cyclamen's local "
+                             f"observation and memory, got variant={self.variant!r}.")
+        if self.discrete:
+            raise ValueError("Learned Option-Critic requires continuous primitive wheel actions. Configure the "
+                             "Cyclamen observation with continuous action spaces before constructing the "
+                             "environment.")
+        self.act_dim = int(self.unwrapped.cfg.action_spaces[self.agents[0]])
+        self.option_state_dim = self.state_dim + cfg.num_options
+        if self.obs_dim != 24:
+            raise ValueError("Learned Option-Critic Phase 2 requires the full 24-channel local sensor vector for "
+                             "its learned motor options. Construct the environment with full_policy_observations "
+                             "enabled.")
+        if self.act_dim != 2:
+            raise ValueError(f"Phase 2 expects the two normalized e-puck wheel commands, got act_dim={self.act_dim}.")
+        self._validate(cfg)
+        torch.set_float32_matmul_precision(cfg.matmul_precision)
+        if self.device.type == "cuda":
+            allow_tf32 = cfg.matmul_precision != "highest"
+            torch.backends.cuda.matmul.allow_tf32 = allow_tf32
+            torch.backends.cudnn.allow_tf32 = allow_tf32
+        if self.comm.rank == 0:
+            print(f"[LearnedOC] envs={self.num_envs}  agents={self.num_agents}  obs={self.obs_dim}  "
+                  f"state={self.state_dim}  wheel_actions={self.act_dim}  options={cfg.num_options}  "
+                  f"decision_period={self.decision_period}")
+
+        # construction order = the reference's (seeded weights match)
+        self.actor = LearnedOptionActor(
+            obs_dim=self.obs_dim, act_dim=self.act_dim, num_options=cfg.num_options, hidden=cfg.hidden_dim,
+            num_layers=cfg.num_layers, memory_size=cfg.memory_size, option_hidden=cfg.option_hidden_dim,
+            option_num_layers=cfg.option_num_layers, option_memory_size=cfg.option_memory_size,
+            initial_termination_probability=cfg.initial_termination_probability,
+            initial_log_std=cfg.initial_log_std, min_log_std=cfg.min_log_std, max_log_std=cfg.max_log_std,
+            option_selector_temperature=cfg.option_selector_temperature, separate_selector=False,
+            epsilon_greedy_selector=True, squash_actions=False).to(self.device)
+        critic = dict(num_agents=self.num_agents, h_size=cfg.critic_hidden_dim, num_heads=cfg.critic_num_heads,
+                      num_layers=cfg.critic_num_layers, memory_size=cfg.memory_size)
+        self.team_critic = POCACritic(self.state_dim, 1, **critic).to(self.device)                     # V(s)
+        self.action_critic = POCACritic(self.option_state_dim, self.act_dim, **critic).to(self.device)  # b_i^U
+        self.option_critic = POCACritic(self.state_dim, cfg.num_options, **critic).to(self.device)     # Q, b^Omega
+        self.actor_parameters = list(self.actor.parameters())
+        self.critic_parameters = (list(self.team_critic.parameters()) + list(self.action_critic.parameters())
+                                  + list(self.option_critic.parameters()))
+        self.params = self.actor_parameters + self.critic_parameters
+        self.fused_optimizer_active = False
+        if cfg.fused_optimizer and self.device.type == "cuda":
+            try:
+                self.actor_optimizer = optim.Adam(self.actor_parameters, lr=cfg.actor_lr, eps=cfg.adam_eps, fused=True)
+                self.critic_optimizer = optim.Adam(self.critic_parameters, lr=cfg.lr, eps=cfg.adam_eps, fused=True)
+                self.fused_optimizer_active = True
+            except (TypeError, RuntimeError) as error:
+                print(f"[LearnedOC] Fused Adam unavailable; using standard Adam ({error})")
+        if not self.fused_optimizer_active:
+            self.actor_optimizer = optim.Adam(self.actor_parameters, lr=cfg.actor_lr, eps=cfg.adam_eps)
+            self.critic_optimizer = optim.Adam(self.critic_parameters, lr=cfg.lr, eps=cfg.adam_eps)
+        self.optimizer = self.critic_optimizer
+        self.actor_comm = self.comm
+        self.critic_comm = TrainerComm(group)
+        self.actor_comm.bind_flat_grads(self.actor_parameters)
+        self.critic_comm.bind_flat_grads(self.critic_parameters)
+        # PPO ratios against an immutable update-start policy (LOT:413-419)
+        self.reference_actor = copy.deepcopy(self.actor).eval()
+        self.reference_actor.requires_grad_(False)
+
+        self.actor_lr_schedule = (PolynomialDecay(cfg.actor_lr, 1e-10, cfg.total_timesteps)
+                                  if cfg.lr_schedule == "linear" else None)
+        self.option_epsilon_schedule = (
+            PolynomialDecay(cfg.option_epsilon_start, cfg.option_epsilon_final,
+                            max(1, int(cfg.total_timesteps * cfg.option_epsilon_decay_fraction)))
+            if cfg.option_epsilon_schedule == "linear" else None)
+        self.termination_prior_schedule = PolynomialDecay(cfg.termination_prior_coef,
+                                                          cfg.termination_prior_final_coef, cfg.total_timesteps)
+        self.option_balance_schedule = PolynomialDecay(cfg.option_balance_coef, cfg.option_balance_final_coef,
+                                                       cfg.total_timesteps)
+        self.current_base_actor_lr = self.current_actor_lr = cfg.actor_lr
+        self.current_option_epsilon = cfg.option_epsilon_start
+        self.current_termination_prior_coef = cfg.termination_prior_coef
+        self.current_option_balance_coef = cfg.option_balance_coef
+        self.actor_lr_scale = 1.0
+
+        self.buffer = LearnedOptionRolloutBuffer(
+            horizon=self._buffer_capacity(), num_envs=self.num_envs, num_agents=self.num_agents,
+            obs_dim=self.obs_dim, state_dim=self.state_dim, act_dim=self.act_dim,
+            memory_size=self.actor.hidden_size, critic_memory_size=self.team_critic.hidden_size, gamma=cfg.gamma,
+            lam=cfg.lam, device=self.device)
+        self.collector = LearnedOptionCollector(
+            env, self.buffer, self.actor, self.team_critic, self.action_critic, self.option_critic,
+            decision_period=self.decision_period, reward_strength=self.reward_strength,
+            num_options=cfg.num_options)
+        self.collector.option_epsilon = self.current_option_epsilon
+        self._rollout_seconds = 0.0
+        if self.comm.rank == 0:
+            print(f"[LearnedOC] Actor params: {sum(p.numel() for p in self.actor.parameters()):,}  Critic params: "
+                  f"team={sum(p.numel() for p in self.team_critic.parameters()):,}  "
+                  f"action={sum(p.numel() for p in self.action_critic.parameters()):,}  "
+                  f"option={sum(p.numel() for p in self.option_critic.parameters()):,}  "
+                  f"fused_adam={self.fused_optimizer_active}")
+
+    @staticmethod
+    def _validate(cfg):
+        """learned_option_critic_trainer.py:234-292."""
+        checks = [
+            (cfg.actor_lr > 0.0, f"actor_lr must be positive, got {cfg.actor_lr}."),
+            (cfg.actor_max_grad_norm > 0.0, f"actor_max_grad_norm must be positive, got {cfg.actor_max_grad_norm}."),
+            (cfg.target_kl >= 0.0, f"target_kl must be non-negative, got {cfg.target_kl}."),
+            (0.0 < cfg.termination_prior_probability < 1.0, "termination_prior_probability must be strictly "
+             f"between 0 and 1, got {cfg.termination_prior_probability}."),
+            (min(cfg.termination_prior_coef, cfg.termination_prior_final_coef) >= 0.0,
+             "termination prior coefficients must be non-negative"),
+            (min(cfg.option_balance_coef, cfg.option_balance_final_coef) >= 0.0,
+             "option balance coefficients must be non-negative"),
+            (0.0 < cfg.actor_lr_scale_min <= 1.0, "actor_lr_scale_min must lie in (0, 1]"),
+            (0.0 <= cfg.option_epsilon_final <= 1.0, "option_epsilon_final must lie in [0, 1]"),
+            (0.0 <= cfg.option_epsilon_start <= 1.0, "option_epsilon_start must lie in [0, 1]"),
+            (cfg.option_epsilon_schedule in ("constant", "linear"), "option_epsilon_schedule must be constant or linear"),
+            (0.0 < cfg.option_epsilon_decay_fraction <= 1.0, "option_epsilon_decay_fraction must lie in (0, 1]"),
+            (cfg.actor_lr_decay_factor > 1.0, "actor_lr_decay_factor must be greater than 1"),
+            (cfg.actor_lr_recovery_factor > 1.0, "actor_lr_recovery_factor must be greater than 1"),
+            (cfg.matmul_precision in ("highest", "high", "medium"),
+             "matmul_precision must be one of highest, high, or medium"),
+        ]
+        for ok, msg in checks:
+            if not ok:
+                raise ValueError(msg)
+
+    # ------------------------------------------------------------ reference attribute surface
+    def __getattr__(self, name):
+        col = self.__dict__.get("collector")
+        if col is not None and name in _COLLECTOR_STATE:
+            return getattr(col, name)
+        raise AttributeError(name)
+
+    def _apply_schedules(self):
+        """learned_option_critic_trainer.py:567-595."""
+        step = self.global_step
+        if self.lr_schedule is not None:
+            self.current_lr = self.lr_schedule.get(step)
+            for group in self.critic_optimizer.param_groups:
+                group["lr"] = self.current_lr
+        base = self.actor_lr_schedule.get(step) if self.actor_lr_schedule is not None else self.cfg.actor_lr
+        self.current_base_actor_lr = base
+        self.current_actor_lr = base * self.actor_lr_scale
+        for group in self.actor_optimizer.param_groups:
+            group["lr"] = self.current_actor_lr
+        if self.eps_schedule is not None:
+            self.current_eps = self.eps_schedule.get(step)
+        if self.beta_schedule is not None:
+            self.current_beta = self.beta_schedule.get(step)
+        self.current_option_epsilon = (self.option_epsilon_schedule.get(step) if self.option_epsilon_schedule
+                                       is not None else self.cfg.option_epsilon_start)
+        self.current_termination_prior_coef = self.termination_prior_schedule.get(step)
+        self.current_option_balance_coef = self.option_balance_schedule.get(step)
+        self.collector.option_epsilon = self.current_option_epsilon
+
+    def _encode_options(self, options: torch.Tensor) -> torch.Tensor:
+        return F.one_hot(options.long(), num_classes=self.cfg.num_options).float()
+
+    def _option_augmented_states(self, states, options):
+        return torch.cat([states, self._encode_options(options)], dim=-1)
+
+    # ------------------------------------------------------------ rollout
+    def collect_rollout(self, obs_dict, rollout_steps: int | None = None, reset_buffer: bool = True):
+        """learned_option_critic_trainer.py:611-954 through the fused decision loop."""
+        steps = self.cfg.horizon if rollout_steps is None else int(rollout_steps)
+        self.collector.option_epsilon = self.current_option_epsilon
+        t0 = time.perf_counter()
+        nxt = self.collector.collect(stack_obs(obs_dict, self.agents), steps, reset_buffer=reset_buffer)
+        self._rollout_seconds += time.perf_counter() - t0
+        self.global_step += self.num_envs * self.num_agents * self.comm.world * steps
+        return {a: nxt[:, i] for i, a in enumerate(self.agents)}
+
+    def _on_train_start(self):
+        self.collector.reset_state()
+
+    # ------------------------------------------------------------ losses
+    @staticmethod
+    def _attention_losses(attentions, loss_mask, dones, d_rows=None, d_pairs=None):
+        """Diversity of the options' attention masks, their temporal change and the mean
+        attention over the active rows (LOT:956-997), as masked sums (no host sync)."""
+        O, D = attentions.shape[-2], attentions.shape[-1]
+        active = loss_mask.to(attentions.dtype)
+        n_rows = d_rows if d_rows is not None else active.sum().clamp_min(1.0)
+        normalized = F.normalize(attentions, p=2, dim=-1, eps=1e-8)
+        sim = torch.matmul(normalized, normalized.transpose(-1, -2))
+        off = ~torch.eye(O, dtype=torch.bool, device=attentions.device)
+        diversity = (sim[..., off].sum(-1) * active).sum() / (n_rows * (O * (O - 1)))
+        pairs = (loss_mask[:, :-1] & loss_mask[:, 1:] & (dones[:, :-1] < 0.5)).to(attentions.dtype)
+        n_pairs = d_pairs if d_pairs is not None else pairs.sum().clamp_min(1.0)
+        delta = (attentions[:, 1:] - attentions[:, :-1]).abs().mean(dim=(-1, -2))
+        temporal = (delta * pairs).sum() / n_pairs
+        mean_attention = (attentions.sum(dim=(-1, -2)) * active).sum() / (n_rows * (O * D))
+        return diversity, temporal, mean_attention
+
+    def _compute_sequence_losses(self, batch: dict, current_eps: float, reference_actor) -> dict:
+        """learned_option_critic_trainer.py:999-1413."""
+        cfg, A, O = self.cfg, self.act_dim, self.cfg.num_options
+        obs, next_obs = batch["obs"], batch["next_obs"]
+        states, next_states = batch["critic_states"], batch["next_critic_states"]
+        options, joint_options = batch["options"], batch["critic_options"]
+        actions, joint_actions = batch["actions"], batch["critic_actions"]
+        loss_mask = batch["loss_mask"].bool()
+        dones = batch["dones"]
+        B, L = obs.shape[:2]
+        N = states.shape[2]
+        boundary = (batch["option_masks"] > 0.5) & loss_mask
+        term_mask = (1.0 - dones) * loss_mask
+        pair_mask = loss_mask[:, :-1] & loss_mask[:, 1:] & (dones[:, :-1] < 0.5)
+        d_mask, d_bound, d_term, d_pairs = self._denominators(
+            [loss_mask.sum(), boundary.sum(), term_mask.sum(), pair_mask.sum()])
+        n_mask = d_mask if d_mask is not None else loss_mask.sum().clamp_min(1)
+        n_mask_f = d_mask if d_mask is not None else loss_mask.to(torch.float32).sum().clamp_min(1.0)
+        n_bound = d_bound if d_bound is not None else boundary.sum().clamp_min(1)
+        n_term = d_term if d_term is not None else term_mask.sum().clamp_min(1)
+
+        mem0 = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
+        (_sel, option_values, _term, action_means, action_stds, attentions,
+         _next) = self.actor.forward_sequence(obs, mem0)
+        with torch.no_grad():
+            ref_out = reference_actor.forward_sequence(obs, (batch["memory_h"].unsqueeze(0),
+                                                             batch["memory_c"].unsqueeze(0)))
+            ref_means, ref_stds = ref_out[3], ref_out[4]
+
+        # AOC: the manager is epsilon-soft over Q_Omega; no selector gradient (LOT:1050-1093)
+        option_dist = self.actor.option_dist(option_values, epsilon=self.current_option_epsilon)
+        new_option_logp = option_dist.log_prob(options)
+        option_entropy = (option_dist.entropy() * boundary).sum() / n_bound
+        sel_w = loss_mask.unsqueeze(-1).to(dtype=option_dist.probs.dtype)
+        marginal = ((option_dist.probs * sel_w).sum(dim=(0, 1)) / sel_w.sum().clamp_min(1.0)).clamp_min(1e-8)
+        option_marginal_entropy = -(marginal * marginal.log()).sum()
+        option_balance_loss = (marginal * (marginal.log() + torch.log(torch.tensor(
+            float(O), device=marginal.device, dtype=marginal.dtype)))).sum()
+        effective_options = option_marginal_entropy.exp()
+        selector_loss = option_values.sum() * 0.0
+        option_approx_kl = option_values.sum() * 0.0
+        behavior_option_logp_error = new_option_logp.sum() * 0.0
+
+        # intra-option wheel policy: PPO against the frozen update-start actor (LOT:1095-1138)
+        action_dist = self.actor.selected_action_dist(action_means, action_stds, options)
+        new_action_logp = action_dist.log_prob(actions)
+        with torch.no_grad():
+            ref_action_logp = reference_actor.selected_action_dist(ref_means, ref_stds, options).log_prob(actions)
+        log_ratio = (new_action_logp - ref_action_logp).clamp(-20.0, 20.0)
+        kl_w = loss_mask.unsqueeze(-1).expand_as(log_ratio).to(log_ratio.dtype)
+        n_kl = n_mask_f * A if d_mask is not None else kl_w.sum().clamp_min(1.0)
+        action_approx_kl = ((log_ratio.exp() - 1.0 - log_ratio) * kl_w).sum() / n_kl
+        behavior_action_logp_error = ((ref_action_logp - batch["old_action_log_probs"]).abs() * kl_w).sum() / n_kl
+        intra_option_loss = stable_trust_region_policy_loss(
+            batch["action_advantages"].reshape(-1, 1).detach(), new_action_logp.reshape(-1, A),
+            ref_action_logp.reshape(-1, A), current_eps, loss_mask.reshape(-1),
+            denom=n_mask_f * A if d_mask is not None else None)
+        action_entropy = (action_dist.entropy().mean(dim=-1) * loss_mask).sum() / n_mask
+
+        # termination logits at s' from the stored post-decision memory (LOT:1140-1169)
+        next_h = batch["next_memory_h"].reshape(B * L, -1).unsqueeze(0).detach()
+        next_c = batch["next_memory_c"].reshape(B * L, -1).unsqueeze(0).detach()
+        (_s, next_option_values, next_term_logits, _m, _sd, _a, _n) = self.actor.step(
+            next_obs.reshape(B * L, self.obs_dim), (next_h, next_c))
+        next_beta_logits = self.actor.selected_termination_logits(next_term_logits, options.reshape(-1)).view(B, L)
+        next_beta = torch.sigmoid(next_beta_logits)
+
+        flat_states = states.reshape(B * L, N, self.state_dim)
+        flat_next_states = next_states.reshape_as(flat_states)
+        flat_joint_options = joint_options.reshape(B * L, N)
+        encoded = self._encode_options(flat_joint_options)
+        flat_joint_actions = joint_actions.reshape(B * L, N, A)
+        option_states = self._option_augmented_states(flat_states, flat_joint_options)
+        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
+        flat_returns = batch["returns"].reshape(-1)
+        flat_mask = loss_mask.reshape(-1)
+        selected_local = option_values.gather(-1, options.unsqueeze(-1)).squeeze(-1).reshape(-1)
+        local_option_value_mean = (selected_local * flat_mask).sum() / (
+            n_mask_f if d_mask is not None else flat_mask.sum().clamp_min(1.0))
+        option_value_spread = (option_values.std(dim=-1, unbiased=False) * loss_mask).sum() / n_mask
+
+        def mem(k):
+            return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
+
+        new_team = self.team_critic.critic_pass(flat_states, mem("team_memory"), sequence_length=L).squeeze(-1)
+        new_action_bl = self.action_critic.focal_baselines(option_states, flat_joint_actions, focal_ids,
+                                                           mem("action_baseline_memory"),
+                                                           sequence_length=L).squeeze(-1)
+        new_joint = self.option_critic.joint_action_pass(flat_states, encoded, mem("option_joint_memory"),
+                                                         sequence_length=L).squeeze(-1)
+        new_option_bl = self.option_critic.focal_baselines(flat_states, encoded, focal_ids,
+                                                           mem("option_baseline_memory"),
+                                                           sequence_length=L).squeeze(-1)
+
+        def tr_loss(new, old_key):
+            return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,
+                                           denom=d_mask)
+
+        value_loss = tr_loss(new_team, "old_team_values")
+        local_option_value_loss = tr_loss(selected_local, "old_local_option_values")
+        action_baseline_loss = tr_loss(new_action_bl, "old_action_baselines")
+        joint_option_value_loss = tr_loss(new_joint, "old_joint_option_values")
+        option_baseline_loss = tr_loss(new_option_bl, "old_option_baselines")
+
+        # arrival-state termination theorem: peers keep their options, the focal robot
+        # compares continuation with V_Omega over its counterfactual alternatives (LOT:1282-1317)
+        with torch.no_grad():
+            next_joint_memory = (batch["next_option_joint_memory_h"].reshape(B * L, -1).unsqueeze(0),
+                                 batch["next_option_joint_memory_c"].reshape(B * L, -1).unsqueeze(0))
+            next_q = self.option_critic.joint_action_pass(flat_next_states, encoded,
+                                                          memory=next_joint_memory).squeeze(-1)
+            alternatives = self.option_critic.focal_discrete_counterfactual_values(
+                flat_next_states, flat_joint_options, focal_ids, O, memory=next_joint_memory)
+            reselection = self.actor.option_state_value(next_option_values, alternatives,
+                                                        epsilon=self.current_option_epsilon)
+            termination_advantage = (next_q - reselection).view(B, L)
+
+        termination_loss = termination_objective(next_beta, termination_advantage, cfg.termination_penalty,
+                                                 term_mask, denom=n_term)
+        prior = F.binary_cross_entropy_with_logits(
+            next_beta_logits, torch.full_like(next_beta_logits, cfg.termination_prior_probability), reduction="none")
+        termination_prior_loss = (prior * term_mask).sum() / n_term
+        termination_entropy = (Bernoulli(logits=next_beta_logits).entropy() * term_mask).sum() / n_term
+        mean_beta = (next_beta * term_mask).sum() / n_term
+        mean_termination_advantage = (termination_advantage * term_mask).sum() / n_term
+        mean_termination_signal = ((termination_advantage + cfg.termination_penalty) * term_mask).sum() / n_term
+        low_sat = ((next_beta < 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
+        high_sat = ((next_beta > 1.0 - 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
+        diversity, temporal, mean_attention = self._attention_losses(
+            attentions, loss_mask, dones, d_mask, d_pairs if d_pairs is not None else None)
+        return {
+            "intra_option_loss": intra_option_loss, "selector_loss": selector_loss,
+            "local_option_value_loss": local_option_value_loss, "local_option_value_mean": local_option_value_mean,
+            "option_value_spread": option_value_spread, "value_loss": value_loss,
+            "action_baseline_loss": action_baseline_loss, "joint_option_value_loss": joint_option_value_loss,
+            "option_baseline_loss": option_baseline_loss, "termination_loss": termination_loss,
+            "action_entropy": action_entropy, "option_entropy": option_entropy,
+            "option_balance_loss": option_balance_loss, "option_marginal_entropy": option_marginal_entropy,
+            "effective_options": effective_options, "termination_entropy": termination_entropy,
+            "termination_prior_loss": termination_prior_loss, "attention_diversity_loss": diversity,
+            "attention_temporal_loss": temporal, "mean_attention": mean_attention, "mean_beta": mean_beta,
+            "mean_termination_advantage": mean_termination_advantage,
+            "mean_termination_signal": mean_termination_signal, "termination_low_saturation": low_sat,
+            "termination_high_saturation": high_sat, "action_approx_kl": action_approx_kl,
+            "option_approx_kl": option_approx_kl, "behavior_action_logp_error": behavior_action_logp_error,
+            "behavior_option_logp_error": behavior_option_logp_error,
+        }
+
+    def compute_losses(self, batch: dict, current_eps: float, reference_actor=None) -> dict:
+        return self._compute_sequence_losses(batch, current_eps, reference_actor or self.reference_actor)
+
+    def objectives(self, losses: dict):
+        """(actor terms dict, actor loss, critic loss) of learned_option_critic_trainer.py:1531-1581."""
+        cfg = self.cfg
+        terms = {
+            "objective_intra_option": cfg.intra_option_coef * losses["intra_option_loss"],
+            "objective_selector": cfg.selector_coef * losses["selector_loss"],
+            "objective_local_option_value": cfg.local_option_value_coef * losses["local_option_value_loss"],
+            "objective_termination": cfg.termination_coef * losses["termination_loss"],
+            "objective_termination_prior": self.current_termination_prior_coef * losses["termination_prior_loss"],
+            "objective_option_balance": self.current_option_balance_coef * losses["option_balance_loss"],
+            "objective_attention_diversity": cfg.attention_diversity_coef * losses["attention_diversity_loss"],
+            "objective_attention_temporal": cfg.attention_temporal_coef * losses["attention_temporal_loss"],
+            "objective_action_entropy": -self.current_beta * losses["action_entropy"],
+            "objective_option_entropy": -cfg.option_entropy_coef * losses["option_entropy"],
+            "objective_termination_entropy": -cfg.termination_entropy_coef * losses["termination_entropy"],
+        }
+        actor_loss = sum(terms.values())
+        critic_loss = (cfg.value_coef * losses["value_loss"] + cfg.action_baseline_coef * losses["action_baseline_loss"]
+                       + cfg.option_value_coef * losses["joint_option_value_loss"]
+                       + cfg.option_baseline_coef * losses["option_baseline_loss"])
+        return terms, actor_loss, critic_loss
+
+    def _clip_step(self, kind: str, loss, comm, optimizer, params, max_norm: float, index: int):
+        comm.zero_grad(optimizer)
+        loss.backward()
+        comm.all_reduce_grads()
+        if self.grad_hook is not None:
+            self.grad_hook((kind, index), params)
+        norm = torch.nn.utils.clip_grad_norm_(params, max_norm, error_if_nonfinite=True)
+        optimizer.step()
+        if self.step_hook is not None:
+            self.step_hook((kind, index), params)
+        return norm
+
+    # ------------------------------------------------------------ update
+    def update(self) -> dict:
+        """learned_option_critic_trainer.py:1421-1765."""
+        cfg = self.cfg
+        self._apply_schedules()
+        T = self.buffer.ptr
+        self.comm.normalize_(self.buffer.action_advantages[:T])
+        dev = self.device
+        totals = torch.zeros(len(METRIC_NAMES) + len(OBJECTIVE_NAMES), dtype=torch.float64, device=dev)
+        grad_norms = torch.zeros(2, dtype=torch.float64, device=dev)
+        samples = torch.zeros((), dtype=torch.float64, device=dev)
+        num_batches = actor_updates = critic_updates = 0
+        max_policy_kl = max_action_kl = max_option_kl = initial_policy_kl = 0.0
+        actor_early_stopped = False
+        self.reference_actor.load_state_dict(self.actor.state_dict())
+        self.reference_actor.eval()
+        for _epoch in range(cfg.num_epochs):
+            for batch in self._sequence_batches():
+                samples += batch["loss_mask"].sum()
+                losses = self.compute_losses(batch, self.current_eps, self.reference_actor)
+                terms, actor_loss, critic_loss = self.objectives(losses)
+                kl = torch.stack([losses["action_approx_kl"].detach(), losses["option_approx_kl"].detach()])
+                if self.comm.active:
+                    kl = self.comm.sum_tensor(kl)     # every rank takes the same early-stop decision
+                host = torch.cat([kl, torch.stack([torch.isfinite(actor_loss.detach()),
+                                                   torch.isfinite(critic_loss.detach())]).to(kl.dtype)]).tolist()
+                action_kl, option_kl = host[0], host[1]
+                policy_kl = max(action_kl, option_kl)
+                if num_batches == 0:
+                    initial_policy_kl = policy_kl
+                    if policy_kl > 1e-6:
+                        raise RuntimeError(f"OC2 update-start policy does not match its frozen reference "
+                                           f"(KL={policy_kl:.6g}).")
+                max_policy_kl = max(max_policy_kl, policy_kl)
+                max_action_kl = max(max_action_kl, action_kl)
+                max_option_kl = max(max_option_kl, option_kl)
+                apply_actor = not actor_early_stopped
+                if apply_actor and cfg.target_kl > 0.0 and policy_kl > 1.5 * cfg.target_kl:
+                    actor_early_stopped, apply_actor = True, False
+                    if self.comm.rank == 0:
+                        print(f"[LearnedOC] Actor PPO early stop: policy KL {policy_kl:.4f} exceeded "
+                              f"{1.5 * cfg.target_kl:.4f}; centralized critics continue")
+                for ok, which in ((host[2], "actor"), (host[3], "critic")):
+                    if not ok:
+                        bad = {n: float(v.detach().cpu()) for n, v in losses.items() if not torch.isfinite(v)}
+                        raise FloatingPointError(f"LearnedOC produced a non-finite {which} loss before backward: "
+                                                 f"{bad}")
+                if apply_actor:
+                    grad_norms[0] += self._clip_step("actor", actor_loss, self.actor_comm, self.actor_optimizer,
+                                                     self.actor_parameters, cfg.actor_max_grad_norm,
+                                                     num_batches).double()
+                    actor_updates += 1
+                grad_norms[1] += self._clip_step("critic", critic_loss, self.critic_comm, self.critic_optimizer,
+                                                 self.critic_parameters, cfg.max_grad_norm, num_batches).double()
+                critic_updates += 1
+                totals += torch.stack([losses[n].detach().reshape(()).double() for n in METRIC_NAMES]
+                                      + [actor_loss.detach().double(), critic_loss.detach().double()]
+                                      + [terms[n].detach().reshape(()).double() for n in OBJECTIVE_NAMES[2:]])
+                num_batches += 1
+        if actor_updates == 0:
+            raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
+                               "should guarantee at least one safe policy minibatch.")
+        modules = (("actor", self.actor), ("team_critic", self.team_critic), ("action_critic", self.action_critic),
+                   ("option_critic", self.option_critic))
+        named = [(f"{m}.{n}", p) for m, mod in modules for n, p in mod.named_parameters()]
+        finite = torch.stack([torch.isfinite(p).all() for _, p in named]).tolist()
+        bad = [n for (n, _), ok in zip(named, finite) if not ok]
+        if bad:
+            raise FloatingPointError("LearnedOC optimizer produced non-finite parameters: " + ", ".join(bad[:10]))
+        self.update_count += 1
+        return self._update_metrics(totals, grad_norms, samples, num_batches, actor_updates, critic_updates,
+                                    max_policy_kl, max_action_kl, max_option_kl, initial_policy_kl,
+                                    actor_early_stopped)
+
+    def _update_metrics(self, totals, grad_norms, samples, num_batches, actor_updates, critic_updates, max_policy_kl,
+                        max_action_kl, max_option_kl, initial_policy_kl, actor_early_stopped) -> dict:
+        """The metrics dict of learned_option_critic_trainer.py:1660-1765 (one host read)."""
+        cfg, buf, T, O = self.cfg, self.buffer, self.buffer.ptr, self.cfg.num_options
+        if self.comm.active:   # gradient norms are already global: every rank clipped the same gradients
+            totals = self.comm.sum_tensor(totals) / self.comm.world
+        dev = totals.device
+        opts = buf.options[:T].reshape(-1)
+        counts = torch.bincount(opts, minlength=O).double()
+        tvalid = (buf.termination_valid[:T] > 0.5).reshape(-1)
+        toh = F.one_hot(buf.termination_options[:T].reshape(-1), O).double() * tvalid.unsqueeze(-1).double()
+        tcount = toh.sum(0)
+        beta_sum = (toh * buf.beta_probs[:T].reshape(-1, 1).double()).sum(0)
+        switch_sum = (toh * buf.option_masks[:T].reshape(-1, 1).double()).sum(0)
+        acts = buf.actions[:T]
+        stats = torch.stack([buf.option_masks[:T].double().sum(), torch.tensor(float(buf.option_masks[:T].numel()),
+                                                                               dtype=torch.float64, device=dev),
+                             (acts.clamp(-3.0, 3.0) / 3.0).abs().double().sum(), acts.abs().double().sum(),
+                             (acts.abs() > 3.0).double().sum(),
+                             torch.tensor(float(acts.numel()), dtype=torch.float64, device=dev)])
+        per = torch.cat([counts, tcount, beta_sum, switch_sum, stats, samples.reshape(1)])
+        if self.comm.active:
+            per = self.comm.sum_tensor(per)
+        n = max(num_batches, 1)
+        flat = (totals / n).tolist() + grad_norms.tolist() + per.tolist() + \
+            self.actor.option_log_stds().detach().exp().mean(dim=-1).tolist()
+        k = len(METRIC_NAMES) + len(OBJECTIVE_NAMES)
+        metrics = dict(zip(METRIC_NAMES + OBJECTIVE_NAMES, flat[:k]))
+        actor_norm_total, critic_norm_total = flat[k], flat[k + 1]
+        p = flat[k + 2:]
+        counts_l, tcount_l, beta_l, switch_l = p[:O], p[O:2 * O], p[2 * O:3 * O], p[3 * O:4 * O]
+        sw_sum, sw_n, abs_act, abs_raw, clipped, n_act, optimizer_samples = p[4 * O:4 * O + 7]
+        option_stds = p[4 * O + 7:]
+        switch_rate = sw_sum / max(sw_n, 1.0)
+        applied_lr, applied_scale = self.current_actor_lr, self.actor_lr_scale
+        adjustment = 0.0
+        if cfg.adaptive_actor_lr and cfg.target_kl > 0.0:
+            if actor_early_stopped or max_policy_kl > cfg.target_kl:
+                self.actor_lr_scale /= cfg.actor_lr_decay_factor
+            elif max_policy_kl < cfg.target_kl / 3.0:
+                self.actor_lr_scale *= cfg.actor_lr_recovery_factor
+            self.actor_lr_scale = min(1.0, max(cfg.actor_lr_scale_min, self.actor_lr_scale))
+            adjustment = 1.0 if self.actor_lr_scale > applied_scale else (-1.0 if self.actor_lr_scale < applied_scale
+                                                                          else 0.0)
+        total_counts = max(sum(counts_l), 1.0)
+        metrics.update({
+            "lr": self.current_lr, "base_actor_lr": self.current_base_actor_lr, "actor_lr": applied_lr,
+            "actor_lr_scale": applied_scale, "next_actor_lr_scale": self.actor_lr_scale,
+            "actor_lr_adjustment": adjustment, "adaptation_policy_kl": max_policy_kl, "eps": self.current_eps,
+            "option_epsilon": self.current_option_epsilon, "beta": self.current_beta,
+            "termination_prior_coef": self.current_termination_prior_coef,
+            "option_balance_coef": self.current_option_balance_coef,
+            "gradient_norm": actor_norm_total / max(actor_updates, 1),
+            "critic_gradient_norm": critic_norm_total / max(critic_updates, 1),
+            "max_policy_kl": max_policy_kl, "max_action_kl": max_action_kl, "max_option_kl": max_option_kl,
+            "initial_policy_kl": initial_policy_kl, "kl_early_stop": float(actor_early_stopped),
+            "actor_updates": float(actor_updates), "critic_updates": float(critic_updates),
+            "optimizer_samples": optimizer_samples, "actor_update_fraction": actor_updates / max(num_batches, 1),
+            "switch_rate": switch_rate, "mean_option_duration": 1.0 / max(switch_rate, 1e-8),
+            "mean_abs_action": abs_act / max(n_act, 1.0), "mean_abs_raw_action": abs_raw / max(n_act, 1.0),
+            "action_clipping": clipped / max(n_act, 1.0), "option_stds": option_stds,
+            "option_betas": [b / c if c > 0 else 0.0 for b, c in zip(beta_l, tcount_l)],
+            "option_switch_rates": [s / c if c > 0 else 0.0 for s, c in zip(switch_l, tcount_l)],
+            "option_termination_counts": [int(c) for c in tcount_l],
+            "option_usage": [c / total_counts for c in counts_l],
+        })
+        return metrics
+
+    # ------------------------------------------------------------ train / logging
+    def _post_update(self, metrics: dict, update_seconds: float, step_delta: int):
+        """learned_option_critic_trainer.py:1843-1876: timings + per-update diagnostics."""
+        rollout_s = self._rollout_seconds
+        self._rollout_seconds = 0.0
+        metrics.update({"rollout_seconds": rollout_s, "update_seconds": update_seconds,
+                        "rollout_sps": step_delta / max(rollout_s, 1e-9),
+                        "optimizer_samples_per_second": metrics["optimizer_samples"] / max(update_seconds, 1e-9)})
+        self._write_update_diagnostics(metrics)
+
+    def _postfix(self, metrics: dict, sps: float) -> dict:
+        return {"act": f"{metrics['intra_option_loss']:.3f}", "q": f"{metrics['local_option_value_loss']:.3f}",
+                "term": f"{metrics['termination_loss']:.3f}", "sw": f"{metrics['switch_rate']:.2f}",
+                "kl": f"{metrics['max_policy_kl']:.3f}", "kl_stop": int(metrics["kl_early_stop"]),
+                "actor_frac": f"{metrics['actor_update_fraction']:.2f}", "SPS": f"{sps:.0f}"}
+
+    UPDATE_SCALARS = {
+        "Update/Max Policy KL": "max_policy_kl", "Update/Adaptation Policy KL": "adaptation_policy_kl",
+        "Update/KL Early Stop": "kl_early_stop", "Update/Actor Update Fraction": "actor_update_fraction",
+        "Update/Base Actor Learning Rate": "base_actor_lr", "Update/Actor Learning Rate": "actor_lr",
+        "Update/Actor Learning Rate Scale": "actor_lr_scale",
+        "Update/Next Actor Learning Rate Scale": "next_actor_lr_scale",
+        "Update/Actor LR Adjustment": "actor_lr_adjustment", "Update/Mean Termination Probability": "mean_beta",
+        "Update/Mean Termination Signal": "mean_termination_signal",
+        "Update/Termination Low Saturation": "termination_low_saturation",
+        "Update/Termination Prior Loss": "termination_prior_loss", "Update/Effective Options": "effective_options",
+        "Update/Option Balance Loss": "option_balance_loss", "Update/Switch Rate": "switch_rate",
+        "Objectives/Actor Total": "actor_objective", "Objectives/Critic Total": "critic_objective",
+        "Objectives/Intra-Option Policy": "objective_intra_option", "Objectives/Option Selector": "objective_selector",
+        "Objectives/Local Option Value": "objective_local_option_value",
+        "Objectives/Termination": "objective_termination", "Objectives/Termination Prior": "objective_termination_prior",
+        "Objectives/Option Balance": "objective_option_balance",
+        "Objectives/Attention Diversity": "objective_attention_diversity",
+        "Objectives/Attention Temporal": "objective_attention_temporal",
+        "Objectives/Action Entropy": "objective_action_entropy", "Objectives/Option Entropy": "objective_option_entropy",
+        "Objectives/Termination Entropy": "objective_termination_entropy",
+        "Performance/Rollout Seconds": "rollout_seconds", "Performance/Update Seconds": "update_seconds",
+        "Performance/Rollout SPS": "rollout_sps",
+        "Performance/Optimizer Samples Per Second": "optimizer_samples_per_second",
+    }
+    SUMMARY_SCALARS = {
+        "Losses/Intra-Option Policy Loss": "intra_option_loss", "Losses/Option Selector Loss": "selector_loss",
+        "Losses/Local Attended Option Value": "local_option_value_loss", "Losses/Value Loss": "value_loss",
+        "Losses/Counterfactual Action Baseline Loss": "action_baseline_loss",
+        "Losses/Collective Option Value Loss": "joint_option_value_loss",
+        "Losses/Counterfactual Option Baseline Loss": "option_baseline_loss",
+        "Losses/Termination Loss": "termination_loss", "Losses/Termination Prior": "termination_prior_loss",
+        "Losses/Option Balance": "option_balance_loss", "Losses/Attention Diversity": "attention_diversity_loss",
+        "Losses/Attention Temporal": "attention_temporal_loss", "Policy/Intra-Option Wheel Entropy": "action_entropy",
+        "Policy/Option Entropy At Boundaries": "option_entropy",
+        "Policy/Option Marginal Entropy": "option_marginal_entropy", "Policy/Effective Options": "effective_options",
+        "Policy/Termination Entropy": "termination_entropy", "Policy/Mean Attention": "mean_attention",
+        "Policy/Local Option Value Mean": "local_option_value_mean",
+        "Policy/Local Option Value Spread": "option_value_spread",
+        "Policy/Mean Termination Probability": "mean_beta",
+        "Policy/Mean Termination Advantage": "mean_termination_advantage",
+        "Policy/Mean Termination Signal": "mean_termination_signal",
+        "Policy/Termination Low Saturation": "termination_low_saturation",
+        "Policy/Termination High Saturation": "termination_high_saturation", "Policy/Switch Rate": "switch_rate",
+        "Policy/Mean Option Duration Decisions": "mean_option_duration",
+        "Policy/Mean Absolute Wheel Action": "mean_abs_action",
+        "Policy/Mean Absolute Raw Wheel Action": "mean_abs_raw_action",
+        "Policy/Wheel Action Clipping": "action_clipping", "Policy/Learning Rate": "lr",
+        "Policy/Base Actor Learning Rate": "base_actor_lr", "Policy/Actor Learning Rate": "actor_lr",
+        "Policy/Actor Learning Rate Scale": "actor_lr_scale",
+        "Policy/Next Actor Learning Rate Scale": "next_actor_lr_scale",
+        "Policy/Termination Prior Coef": "termination_prior_coef", "Policy/Option Balance Coef": "option_balance_coef",
+        "Policy/PPO Clip Epsilon": "eps", "Policy/Option Epsilon": "option_epsilon", "Policy/Beta": "beta",
+        "Diagnostics/Gradient Norm Before Clip": "gradient_norm",
+        "Diagnostics/Actor Gradient Norm Before Clip": "gradient_norm",
+        "Diagnostics/Critic Gradient Norm Before Clip": "critic_gradient_norm",
+        "Diagnostics/Max Policy KL": "max_policy_kl", "Diagnostics/Adaptation Policy KL": "adaptation_policy_kl",
+        "Diagnostics/Actor LR Adjustment": "actor_lr_adjustment", "Diagnostics/Max Action KL": "max_action_kl",
+        "Diagnostics/Max Option KL": "max_option_kl", "Diagnostics/Initial Policy KL": "initial_policy_kl",
+        "Diagnostics/KL Early Stop": "kl_early_stop", "Diagnostics/Actor Updates Applied": "actor_updates",
+        "Diagnostics/Critic Updates Applied": "critic_updates", "Diagnostics/Optimizer Samples": "optimizer_samples",
+        "Diagnostics/Actor Update Fraction": "actor_update_fraction",
+        "Diagnostics/Behavior Action Log Prob Error": "behavior_action_logp_error",
+        "Diagnostics/Behavior Option Log Prob Error": "behavior_option_logp_error",
+    }
+
+    def _write_update_diagnostics(self, metrics: dict):
+        """learned_option_critic_trainer.py:1913-1973 (every update)."""
+        for tag, name in self.UPDATE_SCALARS.items():
+            self.writer.add_scalar(tag, metrics[name], self.global_step)
+
+    def _log(self, metrics: dict, sps: float, mean_rollout_reward: float):
+        """learned_option_critic_trainer.py:1975-2141."""
+        w, s, T = self.writer, self.global_step, self.buffer.ptr
+        for tag, name in self.SUMMARY_SCALARS.items():
+            w.add_scalar(tag, metrics[name], s)
+        for o, usage in enumerate(metrics["option_usage"]):
+            w.add_scalar(f"Policy/Option Usage/{o}", usage, s)
+        for o, std in enumerate(metrics["option_stds"]):
+            w.add_scalar(f"Policy/Intra-Option Std/{o}", std, s)
+        for o, count in enumerate(metrics["option_termination_counts"]):
+            if count > 0:
+                w.add_scalar(f"Policy/Termination Probability/{o}", metrics["option_betas"][o], s)
+                w.add_scalar(f"Policy/Option Switch Rate/{o}", metrics["option_switch_rates"][o], s)
+        stats = torch.stack([self.buffer.rewards[:T].mean(), self.buffer.team_values[:T].mean()]).tolist()
+        w.add_scalar("Policy/Extrinsic Reward", stats[0], s)
+        w.add_scalar("Policy/Extrinsic Value Estimate", stats[1], s)
+        w.add_scalar("Extra/SPS", sps, s)
+        w.add_scalar("Extra/Mean Rollout Reward", mean_rollout_reward, s)
+        w.add_scalar("Extra/Rolling Avg Rollout Reward",
+                     sum(self._rollout_reward_history) / len(self._rollout_reward_history), s)
+        self._log_episodes(w, s)
+
+    # ------------------------------------------------------------ checkpoints
+    def checkpoint_dict(self) -> dict:
+        """learned_option_critic_trainer.py:2143-2237, key for key."""
+        c = self.cfg
+        return {
+            "trainer_type": "learned_option_critic", "option_critic_phase": 2,
+            "learned_option_critic_version": self.CHECKPOINT_VERSION,
+            "training_checkpoint_version": self.TRAINING_CHECKPOINT_VERSION,
+            "paper_parity_version": PAPER_PARITY_VERSION, "fixed_options": False, "learned_options": True,
+            "collective_counterfactual": True, "attention_options": True,
+            "attention_conditioned_outputs": ["local_option_value", "intra_option_policy", "termination"],
+            "option_selection": "epsilon_soft_attended_option_values", "separate_selector_value_heads": False,
+            "primitive_action_space": "continuous_wheels", "action_distribution": "mlagents_normal",
+            "action_transform": "clip_minus3_3_divide3", "variant": self.variant,
+            "actor": self.actor.state_dict(), "team_critic": self.team_critic.state_dict(),
+            "action_critic": self.action_critic.state_dict(), "option_critic": self.option_critic.state_dict(),
+            "actor_optimizer": self.actor_optimizer.state_dict(),
+            "critic_optimizer": self.critic_optimizer.state_dict(),
+            "global_step": self.global_step, "update_count": self.update_count, "actor_lr_scale": self.actor_lr_scale,
+            "seed": c.seed, "hidden_dim": c.hidden_dim, "num_layers": c.num_layers, "recurrent": True,
+            "memory_size": c.memory_size, "memory_size_semantics": "mlagents_total",
+            "lstm_hidden_size": self.actor.manager_hidden_size, "actor_packed_memory_size": self.actor.hidden_size,
+            "sequence_length": c.sequence_length, "option_hidden_dim": c.option_hidden_dim,
+            "option_num_layers": c.option_num_layers, "option_memory_size": c.option_memory_size,
+            "option_recurrent_size": self.actor.option_recurrent_size,
+            "initial_termination_probability": c.initial_termination_probability,
+            "initial_log_std": c.initial_log_std, "min_log_std": c.min_log_std, "max_log_std": c.max_log_std,
+            "option_selector_temperature": c.option_selector_temperature,
+            "option_epsilon_start": c.option_epsilon_start, "option_epsilon_final": c.option_epsilon_final,
+            "option_epsilon_schedule": c.option_epsilon_schedule,
+            "option_epsilon_decay_fraction": c.option_epsilon_decay_fraction,
+            "current_option_epsilon": self.current_option_epsilon, "actor_learning_rate": c.actor_lr,
+            "critic_learning_rate": c.lr, "actor_max_grad_norm": c.actor_max_grad_norm,
+            "max_grad_norm": c.max_grad_norm, "target_kl": c.target_kl, "adaptive_actor_lr": c.adaptive_actor_lr,
+            "actor_lr_scale_min": c.actor_lr_scale_min, "actor_lr_decay_factor": c.actor_lr_decay_factor,
+            "actor_lr_recovery_factor": c.actor_lr_recovery_factor, "fused_optimizer": self.fused_optimizer_active,
+            "matmul_precision": c.matmul_precision, "termination_prior_probability": c.termination_prior_probability,
+            "termination_prior_coef": c.termination_prior_coef,
+            "termination_prior_final_coef": c.termination_prior_final_coef,
+            "option_balance_coef": c.option_balance_coef, "option_balance_final_coef": c.option_balance_final_coef,
+            "critic_hidden_dim": c.critic_hidden_dim, "critic_num_layers": c.critic_num_layers,
+            "critic_num_heads": c.critic_num_heads, "decision_period": self.decision_period, "discrete": False,
+            "num_actions": self.act_dim, "num_options": c.num_options, "act_dim": self.act_dim,
+            "state_dim": self.state_dim, "obs_dim": self.obs_dim,
+        }
+
+    def load_checkpoint(self, path):
+        """learned_option_critic_trainer.py:2240-2327 (weights_only load)."""
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        if ck.get("trainer_type") != "learned_option_critic":
+            raise RuntimeError("Checkpoint is not a learned Option-Critic Phase 2 model.")
+        version = int(ck.get("learned_option_critic_version", 0))
+        if version != self.CHECKPOINT_VERSION:
+            raise RuntimeError(f"Checkpoint uses learned Option-Critic version {version}; this trainer expects "
+                               f"version {self.CHECKPOINT_VERSION}. The paper-aligned epsilon-soft Q_Omega manager "
+                               "requires fresh training.")
+        training_version = int(ck.get("training_checkpoint_version", 0))
+        if training_version != self.TRAINING_CHECKPOINT_VERSION:
+            raise RuntimeError(f"Checkpoint uses a legacy OC2 training layout (version {training_version}); this "
+                               f"trainer expects version {self.TRAINING_CHECKPOINT_VERSION}. The corrected "
+                               "Attention Option-Critic objective requires a fresh training run.")
+        parity = int(ck.get("paper_parity_version", 0))
+        if parity != PAPER_PARITY_VERSION:
+            raise RuntimeError(f"Refusing to resume a parity-v{parity} OC2 checkpoint with the "
+                               f"parity-v{PAPER_PARITY_VERSION} trainer. The environment cadence or training "
+                               "semantics differ; start a fresh run.")
+        if (bool(ck.get("discrete", False)) or ck.get("primitive_action_space") != "continuous_wheels"
+                or ck.get("action_distribution") != "mlagents_normal"
+                or ck.get("action_transform") != "clip_minus3_3_divide3"):
+            raise RuntimeError("Checkpoint is not an OC2 continuous learned-options model. Phase 2 requires six "
+                               "learned intra-option wheel policies; predefined behavior-module checkpoints cannot "
+                               "be resumed.")
+        expected = {"obs_dim": self.obs_dim, "act_dim": self.act_dim, "num_options": self.cfg.num_options}
+        mismatches = {k: (ck.get(k), v) for k, v in expected.items() if int(ck.get(k, -1)) != int(v)}
+        if mismatches:
+            raise RuntimeError(f"OC2 checkpoint/environment layout mismatch: {mismatches}.")
+        self.actor.load_state_dict(ck["actor"])
+        self.team_critic.load_state_dict(ck["team_critic"])
+        self.action_critic.load_state_dict(ck["action_critic"])
+        self.option_critic.load_state_dict(ck["option_critic"])
+        self.actor_optimizer.load_state_dict(ck["actor_optimizer"])
+        self.critic_optimizer.load_state_dict(ck["critic_optimizer"])
+        if self.actor_comm.flat_grad is not None:
+            self.actor_comm.bind_flat_grads(self.actor_parameters)
+            self.critic_comm.bind_flat_grads(self.critic_parameters)
+        self.global_step = int(ck["global_step"])
+        self.update_count = int(ck["update_count"])
+        self.actor_lr_scale = float(ck.get("actor_lr_scale", 1.0))
+        # resume periodic work at the first boundary after the restored step (LOT:2313-2323)
+        if self.cfg.checkpoint_interval > 0:
+            self._next_checkpoint_step = (self.global_step // self.cfg.checkpoint_interval + 1) * \
+                self.cfg.checkpoint_interval
+        if self.cfg.summary_freq > 0:
+            self._next_summary_step = (self.global_step // self.cfg.summary_freq + 1) * self.cfg.summary_freq
+        print(f"[{self.algo}] Loaded <- {path} (step {self.global_step})")

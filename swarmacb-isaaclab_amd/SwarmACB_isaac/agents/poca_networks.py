@@ -422,22 +422,47 @@ class POCACritic(nn.Module):
                              all_actions[keep].view(B, N - 1, self.act_dim), memory, sequence_length,
                              return_memory)
 
-    def value_and_baselines(self, all_states, all_actions, memory=None, baseline_memory=None):
-        """(critic_pass(states, memory, return_memory=True), all_baselines(states, actions,
-        baseline_memory, return_memory=True)) — the two critic calls of a rollout decision
-        (poca_trainer.py:519-548). On the fused path the state-entity rows are embedded,
-        normalised and projected once for both (swarm_rsa_pool SINGLE_OF_PAIRS + BASELINES)."""
+    def decision_passes(self, all_states, all_actions, *, value: bool = True, joint: bool = False,
+                        baselines: bool = True, value_memory=None, joint_memory=None, baseline_memory=None):
+        """The per-decision critic calls of the trainers' rollouts on ONE decision's entities:
+        V(s) = critic_pass(states, value_memory, return_memory=True), Q(s, a) =
+        joint_action_pass(states, actions, joint_memory, return_memory=True) and the baselines
+        all_baselines(states, actions, baseline_memory, return_memory=True)
+        (poca_trainer.py:519-548, option_critic_trainer.py:330-352,
+        learned_option_critic_trainer.py:766-789). Returns a 3-tuple with None for the passes
+        not asked for. On the fused path the 2N entity rows of an env are embedded,
+        normalised and projected ONCE and every pass is one swarm_rsa_pool launch over them
+        (SINGLE_OF_PAIRS, ACTIONS_OF_PAIRS, BASELINES)."""
         B, N, _ = all_states.shape
+        if not (joint or baselines):
+            return (self.critic_pass(all_states, value_memory, return_memory=True) if value else None), None, None
         if not self._fused(all_states, N):
-            return (self.critic_pass(all_states, memory, return_memory=True),
-                    self.all_baselines(all_states, all_actions, baseline_memory, return_memory=True))
+            return (self.critic_pass(all_states, value_memory, return_memory=True) if value else None,
+                    self.joint_action_pass(all_states, all_actions, joint_memory, return_memory=True)
+                    if joint else None,
+                    self.all_baselines(all_states, all_actions, baseline_memory, return_memory=True)
+                    if baselines else None)
         obs_emb = self.obs_entity_enc(all_states)
         act_emb = self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1))
-        pooled_v, pooled_b = _fused_rsa(self.self_attn, torch.cat([obs_emb, act_emb], dim=1),
-                                        (_native.RSA_SINGLE_OF_PAIRS, _native.RSA_BASELINES), N)
-        value = self._value_tail(pooled_v, N, memory, 1, True)
-        bl, next_bm = self._value_tail(pooled_b, N, baseline_memory, 1, True)
-        return value, (bl.squeeze(-1).reshape(B, N), next_bm)
+        modes = [m for m, on in ((_native.RSA_SINGLE_OF_PAIRS, value), (_native.RSA_ACTIONS_OF_PAIRS, joint),
+                                 (_native.RSA_BASELINES, baselines)) if on]
+        pooled = list(_fused_rsa(self.self_attn, torch.cat([obs_emb, act_emb], dim=1), tuple(modes), N))
+        out = []
+        for on, mem in ((value, value_memory), (joint, joint_memory)):
+            out.append(self._value_tail(pooled.pop(0), N, mem, 1, True) if on else None)
+        if baselines:
+            bl, next_bm = self._value_tail(pooled.pop(0), N, baseline_memory, 1, True)
+            out.append((bl.squeeze(-1).reshape(B, N), next_bm))
+        else:
+            out.append(None)
+        return tuple(out)
+
+    def value_and_baselines(self, all_states, all_actions, memory=None, baseline_memory=None):
+        """(critic_pass(states, memory, return_memory=True), all_baselines(states, actions,
+        baseline_memory, return_memory=True)) — the two critic calls of a POCA rollout
+        decision (poca_trainer.py:519-548), through decision_passes."""
+        v, _, b = self.decision_passes(all_states, all_actions, value_memory=memory, baseline_memory=baseline_memory)
+        return v, b
 
     def all_baselines(self, all_states, all_actions, memory=None, sequence_length: int = 1,
                       return_memory: bool = False):

@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
     constexpr int DH = HD / NH;   // head width
     const bool single = mode != SWARM_RSA_BASELINES;
     const int erows = mode == SWARM_RSA_SINGLE ? N : 2 * N;   // entity rows per env in memory
+    const int roff = mode == SWARM_RSA_ACTIONS_OF_PAIRS ? N : 0;  // first staged row of an env's block
     const int iters = single ? (B + SINGLE_ENVS - 1) / SINGLE_ENVS : B;
 
     __shared__ float Xs[RMAX * LDSW];
@@ -116,17 +117,18 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
         const int G = R / groups;
         const size_t out0 = single ? (size_t)e0 : (size_t)e0 * N;
         // ---- phase 0: x, q, k, v rows of this iteration
-        // (SINGLE_OF_PAIRS: staged row r is row r % N of env e0 + r / N's 2N-row block)
+        // (SINGLE_OF_PAIRS: staged row r is row r % N of env e0 + r / N's 2N-row block;
+        //  ACTIONS_OF_PAIRS: row N + r % N of that block)
         const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)e0 * erows * HD);
         const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)e0 * erows * 3 * HD);
         for (int i = tid; i < R * (HD / 4); i += NT) {
             const int r = i / (HD / 4), c4 = i % (HD / 4);
-            const int mr = single ? (r / N) * erows + (r - (r / N) * N) : r;
+            const int mr = single ? (r / N) * erows + roff + (r - (r / N) * N) : r;
             *reinterpret_cast<float4*>(&Xs[r * LDSW + 4 * c4]) = x4[mr * (HD / 4) + c4];
         }
         for (int i = tid; i < R * (3 * HD / 4); i += NT) {
             const int r = i / (3 * HD / 4), c4 = i % (3 * HD / 4), c = 4 * c4;
-            const int mr = single ? (r / N) * erows + (r - (r / N) * N) : r;
+            const int mr = single ? (r / N) * erows + roff + (r - (r / N) * N) : r;
             float* dst = c < HD ? &Qs[r * LDSW + c] : c < 2 * HD ? &Ks[r * LDSW + c - HD] : &Vs[r * LDSW + c - 2 * HD];
             *reinterpret_cast<float4*>(dst) = q4[mr * (3 * HD / 4) + c4];
         }
@@ -350,7 +352,8 @@ extern "C" {
 
 int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,
                        const float* qkv, const float* w_out, const float* b_out, float* pooled, void* stream) {
-    if (mode != SWARM_RSA_SINGLE && mode != SWARM_RSA_BASELINES && mode != SWARM_RSA_SINGLE_OF_PAIRS)
+    if (mode != SWARM_RSA_SINGLE && mode != SWARM_RSA_BASELINES && mode != SWARM_RSA_SINGLE_OF_PAIRS &&
+        mode != SWARM_RSA_ACTIONS_OF_PAIRS)
         return SWARM_ERR_ARG;
     if (hidden != HD || B < 0 || N < 1 || N > NMAX) return SWARM_ERR_ARG;
     if (heads != 1 && heads != 2 && heads != 4) return SWARM_ERR_ARG;

@@ -47,15 +47,16 @@ class ReplayEnv:
     (make_glue_golden.ScriptedEnv semantics), behind the env surface the
     collectors use."""
 
-    def __init__(self, fx, device):
+    def __init__(self, fx, device, discrete: bool = True):
         E, N, D, R, dp = (int(x) for x in fx["meta"])
         dev = torch.device(device)
         self.num_envs, self.num_agents, self.device = E, N, dev
         self.unwrapped = self
         self.scene = types.SimpleNamespace(num_envs=E)
         agents = [f"epuck_{i}" for i in range(N)]
-        self.cfg = types.SimpleNamespace(num_agents=N, discrete_actions=True, num_actions=6, variant="cyclamen",
-                                         possible_agents=agents, action_spaces={a: 2 for a in agents})
+        self.cfg = types.SimpleNamespace(num_agents=N, discrete_actions=discrete, num_actions=6,
+                                         variant="cyclamen", possible_agents=agents,
+                                         action_spaces={a: 2 for a in agents})
         self.possible_agents = agents
         self.max_episode_length = 1200
         g = lambda k: torch.as_tensor(np.ascontiguousarray(fx[k])).to(dev)  # noqa: E731

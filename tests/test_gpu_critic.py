@@ -117,7 +117,7 @@ def test_rejects_unsupported_shapes(gpu_device):
     assert lib.swarm_rsa_pool(0, 1, 21, 4, 128, p, p, p, p, p, None) == -1   # N > 20
     assert lib.swarm_rsa_pool(0, 1, 20, 8, 128, p, p, p, p, p, None) == -1   # 8 heads
     assert lib.swarm_rsa_pool(0, 1, 20, 4, 256, p, p, p, p, p, None) == -1   # hidden 256
-    assert lib.swarm_rsa_pool(3, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode
+    assert lib.swarm_rsa_pool(4, 1, 20, 4, 128, p, p, p, p, p, None) == -1   # mode
 
 
 @pytest.mark.parametrize("B,N,heads", [(1, 20, 4), (7, 20, 2), (5, 13, 4), (9, 3, 1), (2, 1, 4)])
@@ -232,3 +232,30 @@ def test_value_and_baselines_shares_rows(gpu_device, fused_calls, memory):
     if memory:
         torch.testing.assert_close(vm[0], rvm[0], **TOL)
         torch.testing.assert_close(bm[1], rbm[1], **TOL)
+
+
+@pytest.mark.parametrize("N", [20, 7])
+def test_decision_passes_value_joint_baselines_share_rows(gpu_device, fused_calls, N):
+    """The option-critic decision's three critic calls on one projection pass
+    (SINGLE_OF_PAIRS + ACTIONS_OF_PAIRS + BASELINES) equal critic_pass,
+    joint_action_pass and all_baselines called separately, memories included."""
+    torch.manual_seed(11)
+    E = 515
+    c = PN.POCACritic(5, 6, N, 128, 4, 2, memory_size=128).to(gpu_device).eval()
+    with torch.no_grad():
+        for p in c.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+        s = torch.randn(E, N, 5, device=gpu_device)
+        a = torch.nn.functional.one_hot(torch.randint(0, 6, (E, N), device=gpu_device), 6).float()
+        mem = lambda n: (torch.randn(1, n, 64, device=gpu_device), torch.randn(1, n, 64, device=gpu_device))  # noqa
+        mv, mj, mb = mem(E), mem(E), mem(E * N)
+        (v, vm), (j, jm), (b, bm) = c.decision_passes(s, a, value=True, joint=True, baselines=True,
+                                                      value_memory=mv, joint_memory=mj, baseline_memory=mb)
+        assert fused_calls == [(2, 3, 1)]
+        _, (j2, jm2), _ = c.decision_passes(s, a, value=False, joint=True, baselines=False, joint_memory=mj)
+        rv, rvm = c.critic_pass(s, mv, return_memory=True)
+        rj, rjm = c.joint_action_pass(s, a, mj, return_memory=True)
+        rb, rbm = c.all_baselines(s, a, mb, return_memory=True)
+    for got, ref in ((v, rv), (j, rj), (j2, rj), (b, rb), (vm[0], rvm[0]), (jm[1], rjm[1]), (jm2[0], rjm[0]),
+                     (bm[0], rbm[0])):
+        torch.testing.assert_close(got, ref, **TOL)
