@@ -1,4 +1,4 @@
-"""Headless `scripts/play.py` for POCA checkpoints.
+"""Headless `scripts/play.py` for POCA and both Option-Critic phases.
 
     python -m SwarmACB_isaac.play --checkpoint poca_final.pt [--config cfg.yaml] [--task ID]
         [--variant NAME] [--num_envs 1] [--num_episodes 10] [--deterministic] [--seed 0]
@@ -9,11 +9,14 @@ the variant, the decision period and the env overrides; the checkpoint's
 count (default 1, as in the reference); the task is --task, else the config's
 override, else SwarmACB-DirectionalGate-v0; the env cfg takes the seed, the
 variant and the overrides. Without a config the decision period is 1, as in
-the reference. The actor is rebuilt from the checkpoint (play.py:379-436) and
-evaluated by `agents.checkpoint.evaluate` (play.py:537-705); the summary lines
-of play.py:707-721 are printed. The GUI, viewer and HUD options of the
-reference have no counterpart here (Isaac Sim visuals are out of scope), and
-option-critic checkpoints are refused.
+the reference; a learned Option-Critic (OC2) checkpoint switches the env to
+continuous wheels and 24-D observations (play.py:330-342). The policy is
+rebuilt from the checkpoint (play.py:379-436: POCA actors, the fixed-option
+manager, the learned-option actor) and evaluated by
+`agents.checkpoint.evaluate` (play.py:528-705, call-and-return options with
+the checkpoint's option epsilon and action transform); the summary lines of
+play.py:707-721 are printed. The GUI, viewer and HUD options of the reference
+have no counterpart here (Isaac Sim visuals are out of scope).
 """
 
 from __future__ import annotations
@@ -26,13 +29,14 @@ import sys
 import numpy as np
 import torch
 
-from .agents.checkpoint import OPTION_TRAINERS, actor_from_checkpoint, evaluate, read_checkpoint
+from .agents.checkpoint import actor_from_checkpoint, evaluate, read_checkpoint
 from .agents.config import load_config
 from .registry import cfg_class, make
 
 
 def parse(argv=None):
-    ap = argparse.ArgumentParser(description="Evaluate a POCA checkpoint on the e-puck env (headless)")
+    ap = argparse.ArgumentParser(description="Evaluate a POCA / Option-Critic checkpoint on the e-puck env "
+                                             "(headless)")
     ap.add_argument("--config", type=str, default=None)
     ap.add_argument("--task", type=str, default=None)
     ap.add_argument("--variant", type=str, default=None)
@@ -64,13 +68,14 @@ def resolve(args):
     if variant is None:
         variant = "dandelion"
     task_id = args.task or env_overrides.pop("task", None) or "SwarmACB-DirectionalGate-v0"
-    trainer_type = ckpt.get("trainer_type", "poca")
-    if trainer_type in OPTION_TRAINERS:
-        raise NotImplementedError(f"{trainer_type} checkpoints need the option-critic networks, "
-                                  "which this build does not carry")
     env_cfg = cfg_class(task_id)()
     env_cfg.seed = args.seed
     env_cfg.update_variant(variant)
+    if ckpt.get("trainer_type", "poca") == "learned_option_critic":
+        if bool(ckpt.get("discrete", False)):
+            raise RuntimeError("This checkpoint selects predefined behavior modules and is not a valid OC2 "
+                               "learned-options checkpoint.")
+        env_cfg.use_continuous_actions(full_observations=True)
     for key, value in env_overrides.items():
         if key == "num_envs":
             env_cfg.scene.num_envs = value
@@ -96,7 +101,11 @@ def main(argv=None) -> list[float]:
     print(f"[Play] trainer={info['trainer_type']}  variant={variant}  discrete={info['discrete']}  "
           f"recurrent={info['recurrent']}  hidden={info['hidden_dim']}  layers={info['num_layers']}  "
           f"obs={obs_dim}  decision_period={decision_period}", flush=True)
-    rewards = evaluate(env, actor, args.num_episodes, decision_period, args.deterministic)
+    if args.deterministic and info["trainer_type"] in ("option_critic", "learned_option_critic"):
+        print("[Play] Warning: deterministic Option-Critic playback thresholds termination probabilities at "
+              "0.5. Use stochastic playback to evaluate the learned call-and-return policy.")
+    rewards = evaluate(env, actor, args.num_episodes, decision_period, args.deterministic,
+                       option_epsilon=info["option_epsilon"], action_transform=info["action_transform"])
     print(f"\n{'=' * 50}")
     print(f"Results over {len(rewards)} episodes:")
     print(f"  Mean reward : {statistics.mean(rewards):.2f}")

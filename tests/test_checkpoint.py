@@ -80,7 +80,7 @@ def test_playback_refusals():
     ckpt = CK.poca_checkpoint(actor, critic, obs_dim=obs)
     with pytest.raises(ValueError, match="Recurrent playback"):
         CK.actor_from_checkpoint(dict(ckpt, recurrent=True), obs)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="learned Option-Critic version 0"):
         CK.actor_from_checkpoint(dict(ckpt, trainer_type="learned_option_critic"), obs)
 
 

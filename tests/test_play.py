@@ -65,3 +65,72 @@ def test_play_main_on_gpu(tmp_path, gpu_device):
     r1 = play.main(argv)
     r2 = play.main(argv)
     assert len(r1) == 4 and r1 == r2
+
+
+def _option_checkpoints(tmp_path):
+    """Checkpoints written by this package's OC / OC2 trainers (fixture-sized networks)."""
+    import oc2_fixtures as O2
+    import oc_fixtures as OF
+
+    tr_oc, _, _, _ = OF.make_oc_trainer("oc_update", "cpu")
+    tr_oc2, _, _, _ = O2.make_oc2_trainer("oc2_update", "cpu")
+    paths = {}
+    for kind, tr in (("oc", tr_oc), ("oc2", tr_oc2)):
+        paths[kind] = tmp_path / f"{kind}.pt"
+        torch.save(tr.checkpoint_dict(), paths[kind])
+    return paths, tr_oc, tr_oc2
+
+
+def test_option_checkpoints_rebuild_their_policies(tmp_path):
+    """play.py:379-436 for both Option-Critic phases: the fixed-option manager and the
+    learned-option actor come back with the trainer's weights; an OC2 checkpoint
+    switches the env to continuous wheels and 24-D observations (play.py:330-342)."""
+    paths, tr_oc, tr_oc2 = _option_checkpoints(tmp_path)
+    net, info = CK.actor_from_checkpoint(str(paths["oc"]), 4)
+    assert info["trainer_type"] == "option_critic" and info["num_options"] == 6
+    for (k, v), (k2, v2) in zip(net.state_dict().items(), tr_oc.manager.state_dict().items()):
+        assert k == k2 and torch.equal(v, v2)
+    net2, info2 = CK.actor_from_checkpoint(str(paths["oc2"]), 24)
+    assert info2["action_transform"] == "clip_minus3_3_divide3"
+    for (k, v), (k2, v2) in zip(net2.state_dict().items(), tr_oc2.actor.state_dict().items()):
+        assert k == k2 and torch.equal(v, v2)
+    with pytest.raises(RuntimeError, match="obs_dim=24"):
+        CK.actor_from_checkpoint(str(paths["oc2"]), 4)
+    args = play.parse(["--checkpoint", str(paths["oc2"]), "--task", "SwarmACB-XOR-v0"])
+    task, variant, env_cfg, dp, _ = play.resolve(args)
+    assert variant == "cyclamen" and env_cfg.obs_dim == 24 and not env_cfg.discrete_actions
+    args = play.parse(["--checkpoint", str(paths["oc"]), "--task", "SwarmACB-DirectionalGate-v0"])
+    _, variant, env_cfg, _, _ = play.resolve(args)
+    assert variant == "cyclamen" and env_cfg.obs_dim == 4 and env_cfg.discrete_actions
+
+
+def test_option_playback_policy_call_and_return_on_cpu(tmp_path):
+    """PlaybackPolicy (play.py:528-641): options are drawn where none is set, kept until
+    the termination head fires, reset per finished env; OC2 wheels are clip(-3,3)/3."""
+    paths, _, _ = _option_checkpoints(tmp_path)
+    torch.manual_seed(3)
+    net, info = CK.actor_from_checkpoint(str(paths["oc"]), 4)
+    pol = CK.PlaybackPolicy(net, 3, 4, "cpu", deterministic=True)
+    obs = torch.randn(12, 4)
+    a1 = pol.act(obs)
+    assert a1.shape == (3, 4, 1) and int(a1.min()) >= 0
+    logits, term, _ = net.step(obs, (torch.zeros(1, 12, net.hidden_size), torch.zeros(1, 12, net.hidden_size)))
+    assert torch.equal(a1.view(-1), logits.argmax(-1))          # first decision: every option is new
+    pol.reset_env(1)
+    assert bool((pol.current_options[1] == -1).all()) and not pol.memory[0][:, 4:8].any()
+    net2, info2 = CK.actor_from_checkpoint(str(paths["oc2"]), 24)
+    pol2 = CK.PlaybackPolicy(net2, 3, 4, "cpu", deterministic=False, option_epsilon=info2["option_epsilon"],
+                             action_transform=info2["action_transform"])
+    w = pol2.act(torch.randn(12, 24))
+    assert w.shape == (3, 4, 2) and float(w.abs().max()) <= 1.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,task", [("oc", "SwarmACB-DirectionalGate-v0"), ("oc2", "SwarmACB-XOR-v0")])
+def test_play_option_checkpoints_on_gpu(tmp_path, gpu_device, kind, task):
+    paths, _, _ = _option_checkpoints(tmp_path)
+    argv = ["--checkpoint", str(paths[kind]), "--task", task, "--num_envs", "3", "--num_episodes", "3",
+            "--seed", "5", "--device", str(gpu_device)]
+    r1 = play.main(argv)
+    r2 = play.main(argv)
+    assert len(r1) == 3 and r1 == r2        # seeded stochastic playback is reproducible
