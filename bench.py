@@ -62,6 +62,8 @@ def parse():
                     help="instead of the step: the fused critic attention at C3 (tools/bench_critic.py)")
     ap.add_argument("--collect", action="store_true",
                     help="instead of the step: the whole C3 rollout decision loop (tools/bench_collect.py)")
+    ap.add_argument("--train", action="store_true",
+                    help="instead of the step: the C3/C4/C5 trainers' rollout + update (tools/bench_train.py)")
     args, rest = ap.parse_known_args()
     args.rest = rest
     return args
@@ -166,10 +168,14 @@ def prewarm(seconds: float, E: int, dp: int, dev) -> float:
 
 def main():
     args = parse()
-    if args.rollout or args.critic or args.collect:
+    if args.rollout or args.critic or args.collect or args.train:
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         sys.argv = [sys.argv[0]] + args.rest
-        if args.collect:
+        if args.train:
+            import bench_train
+
+            bench_train.main()
+        elif args.collect:
             import bench_collect
 
             bench_collect.main()
