@@ -1,0 +1,62 @@
+/*
+ * swarmtrain.h — C ABI of the trainer-update kernels in libswarmstep.so.
+ *
+ * The PPO updates of all three trainers unroll an ML-Agents LSTM memory over
+ * `sequence_length`-step sequences of every minibatch:
+ *
+ *   POCATrainer._compute_recurrent_losses     agents/poca_trainer.py:706-723 (per-step loop, state
+ *                                             zeroed after the steps where the episode ended)
+ *   FixedOptionCriticTrainer (manager)        agents/option_critic_trainer.py:496-506 (same loop)
+ *   LearnedOptionActor.forward_sequence       agents/learned_option_critic_networks.py:424-456
+ *                                             (manager + per-option LSTMs over whole sequences)
+ *   POCACritic memory LSTM                    agents/poca_networks.py:596-625 (whole sequences)
+ *
+ * The reference runs torch.nn.LSTM once per time step (the masked loops) or once
+ * per sequence batch: at ML-Agents minibatch sizes (16 sequences x 128 steps)
+ * that is hundreds of tiny library calls per optimizer step. These two kernels
+ * run the whole recurrence of a sequence in ONE workgroup: forward keeps W_hh in
+ * registers and the state in LDS across all T steps, backward (BPTT) walks the
+ * steps in reverse with W_hh^T in registers. The input projection
+ * x W_ih^T + b_ih + b_hh and the weight gradients are plain GEMMs left to the
+ * caller (hipBLASLt through torch).
+ *
+ * Gate order and math are torch.nn.LSTM's (i | f | g | o):
+ *   gates_t = xg_t + W_hh h_{t-1}'    c_t = sig(f) c_{t-1}' + sig(i) tanh(g)    h_t = sig(o) tanh(c_t)
+ * with the carried state masked between steps: h_{t-1}' = keep[t-1] h_{t-1},
+ * c_{t-1}' = keep[t-1] c_{t-1} for t >= 1 (keep = NULL: no masking), and
+ * (h_{-1}', c_{-1}') = (h0, c0).
+ * Conventions as swarmstep.h: caller-owned device pointers, row-major, async on
+ * `stream`, 0 = ok, negative = swarm_status_t. Supported: 1 <= units <= 64.
+ */
+#ifndef SWARMTRAIN_H
+#define SWARMTRAIN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Forward over n sequences of T steps.
+ * xg: [n][T][4 units] input projections (incl. both biases); w_hh: [4 units][units] (torch layout);
+ * h0, c0: [n][units]; keep: [n][T] f32 or NULL.
+ * Outputs: h_out: [n][T][units] (the LSTM output sequence); c_out: [n][T][units] (cell states, kept for
+ * backward); act: [n][T][4 units] post-activation gates sig(i), sig(f), tanh(g), sig(o) (kept for backward). */
+int32_t swarm_lstm_seq_forward(int64_t n, int32_t T, int32_t units, const float* xg, const float* w_hh,
+                               const float* h0, const float* c0, const float* keep, float* h_out, float* c_out,
+                               float* act, void* stream);
+
+/* Backward of swarm_lstm_seq_forward (BPTT) from the saved act / c_out.
+ * dh_out: [n][T][units] gradient of h_out; dh_n, dc_n: [n][units] gradients of the final state
+ * (h_out[:, T-1], c_out[:, T-1]; NULL = 0).
+ * Outputs: dxg: [n][T][4 units] gradient of the gate pre-activations (= of xg; W_hh's gradient is
+ * dxg^T h_prev' and the caller forms it with one GEMM); dh0, dc0: [n][units] (NULL = not needed). */
+int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float* w_hh, const float* c0,
+                                const float* keep, const float* c_out, const float* act, const float* dh_out,
+                                const float* dh_n, const float* dc_n, float* dxg, float* dh0, float* dc0,
+                                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWARMTRAIN_H */

@@ -69,6 +69,8 @@ class GatherField(C.Structure):
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
 CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
+TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward"]
+LSTM_SEQ_MAX_UNITS = 64
 RSA_SINGLE, RSA_BASELINES, RSA_SINGLE_OF_PAIRS, RSA_ACTIONS_OF_PAIRS = 0, 1, 2, 3
 
 RECORD_MAX_MEMORIES = 12
@@ -141,6 +143,10 @@ def load() -> C.CDLL:
     lib.swarm_rsa_embedding_norm.argtypes = [C.c_int64, i32, vp, vp, vp]
     lib.swarm_lstm_cell.restype = i32
     lib.swarm_lstm_cell.argtypes = [C.c_int64, i32, vp, vp, vp, vp, vp]
+    lib.swarm_lstm_seq_forward.restype = i32
+    lib.swarm_lstm_seq_forward.argtypes = [C.c_int64, i32, i32] + [vp] * 9
+    lib.swarm_lstm_seq_backward.restype = i32
+    lib.swarm_lstm_seq_backward.argtypes = [C.c_int64, i32, i32] + [vp] * 12
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -181,7 +181,7 @@ class PlaybackPolicy:
         if self.deterministic:
             terminate = (beta_logits > 0.0).view(self.E, self.N)
         else:
-            terminate = torch.distributions.Bernoulli(logits=beta_logits).sample().bool().view(self.E, self.N)
+            terminate = torch.distributions.Bernoulli(validate_args=False, logits=beta_logits).sample().bool().view(self.E, self.N)
         self.current_options = torch.where(terminate | (self.current_options < 0), proposed.view(self.E, self.N),
                                            self.current_options)
 
@@ -205,13 +205,13 @@ class PlaybackPolicy:
         if self.kind == "option_critic":
             logits, term, nm = net.step(flat_obs, self.memory)
             self.memory = (nm[0], nm[1])
-            proposed = logits.argmax(dim=-1) if det else torch.distributions.Categorical(logits=logits).sample()
+            proposed = logits.argmax(dim=-1) if det else torch.distributions.Categorical(validate_args=False, logits=logits).sample()
             self._switch(proposed, term.gather(-1, self.current_options.clamp(min=0).reshape(-1, 1)).squeeze(-1))
             return self.current_options.unsqueeze(-1)
         if self.kind == "recurrent":
             logits, nm = net.step(flat_obs, self.memory)
             self.memory = (nm[0], nm[1])
-            act = logits.argmax(dim=-1) if det else torch.distributions.Categorical(logits=logits).sample()
+            act = logits.argmax(dim=-1) if det else torch.distributions.Categorical(validate_args=False, logits=logits).sample()
             return act.view(E, N, 1)
         if self.kind == "discrete":
             act = net(flat_obs).argmax(dim=-1) if det else net.get_dist(flat_obs).sample()

@@ -160,7 +160,7 @@ class POCARolloutCollector:
                 buf.memory_c[t].copy_(self.actor_memory_c.squeeze(0).view(E, N, -1))
                 logits, nm = self.actor.step(flat_obs, (self.actor_memory_h, self.actor_memory_c))
                 self.actor_memory_h, self.actor_memory_c = nm[0].detach(), nm[1].detach()
-                dist = torch.distributions.Categorical(logits=logits)
+                dist = torch.distributions.Categorical(validate_args=False, logits=logits)
             else:
                 dist = self.actor.get_dist(flat_obs)
             flat_act = dist.sample()

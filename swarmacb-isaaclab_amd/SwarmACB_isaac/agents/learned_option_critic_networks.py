@@ -48,7 +48,7 @@ class SquashedNormal:
 
     def __init__(self, loc: torch.Tensor, scale: torch.Tensor):
         self.loc, self.scale = loc, scale
-        self.base_dist = Normal(loc, scale)
+        self.base_dist = Normal(loc, scale, validate_args=False)
 
     @property
     def mean(self) -> torch.Tensor:
@@ -250,20 +250,20 @@ class LearnedOptionActor(nn.Module):
     def selected_action_dist(self, action_means, action_stds, options):
         means = self._gather_options(action_means, options)
         stds = self._gather_options(action_stds, options)
-        return SquashedNormal(means, stds) if self.squash_actions else Normal(means, stds)
+        return SquashedNormal(means, stds, validate_args=False) if self.squash_actions else Normal(means, stds, validate_args=False)
 
     def option_dist(self, option_scores: torch.Tensor, epsilon: float = 0.0) -> Categorical:
         """Call-and-return policy over options: epsilon-soft over the attended Q_Omega
         values (AOC), or softmax logits for v2/v3 checkpoints (LON:562-589)."""
         if not self.epsilon_greedy_selector:
-            return Categorical(logits=option_scores / self.option_selector_temperature)
+            return Categorical(validate_args=False, logits=option_scores / self.option_selector_temperature)
         epsilon = float(epsilon)
         if not 0.0 <= epsilon <= 1.0:
             raise ValueError("option epsilon must lie in [0, 1]")
         probs = torch.full_like(option_scores, epsilon / option_scores.shape[-1])
         greedy = option_scores.argmax(dim=-1, keepdim=True)
         probs.scatter_add_(-1, greedy, torch.full_like(greedy, 1.0 - epsilon, dtype=probs.dtype))
-        return Categorical(probs=probs)
+        return Categorical(validate_args=False, probs=probs)
 
     def option_state_value(self, option_scores, option_values, epsilon: float = 0.0) -> torch.Tensor:
         """V_Omega under the epsilon-soft option policy (LON:591-612)."""

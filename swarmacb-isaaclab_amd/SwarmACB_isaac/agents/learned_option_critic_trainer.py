@@ -402,7 +402,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         prior = F.binary_cross_entropy_with_logits(
             next_beta_logits, torch.full_like(next_beta_logits, cfg.termination_prior_probability), reduction="none")
         termination_prior_loss = (prior * term_mask).sum() / n_term
-        termination_entropy = (Bernoulli(logits=next_beta_logits).entropy() * term_mask).sum() / n_term
+        termination_entropy = (Bernoulli(validate_args=False, logits=next_beta_logits).entropy() * term_mask).sum() / n_term
         mean_beta = (next_beta * term_mask).sum() / n_term
         mean_termination_advantage = (termination_advantage * term_mask).sum() / n_term
         mean_termination_signal = ((termination_advantage + cfg.termination_penalty) * term_mask).sum() / n_term

@@ -105,12 +105,12 @@ class FixedOptionCollector:
                 flat_obs, (self.manager_memory_h, self.manager_memory_c))
             self.manager_memory_h, self.manager_memory_c = nm[0], nm[1]
 
-            option_dist = Categorical(logits=option_logits)
+            option_dist = Categorical(validate_args=False, logits=option_logits)
             proposed = self.sample_options(option_dist).view(E, N)
             proposed_logp = option_dist.log_prob(proposed.reshape(-1)).view(E, N)
             force_new = cur < 0
             beta_logits = termination_logits.gather(-1, cur.clamp(min=0).reshape(-1, 1)).squeeze(-1)
-            terminate = self.sample_termination(Bernoulli(logits=beta_logits)).bool().view(E, N)
+            terminate = self.sample_termination(Bernoulli(validate_args=False, logits=beta_logits)).bool().view(E, N)
             switch = terminate | force_new
             torch.where(switch, proposed, cur, out=cur)
             buf.options[t].copy_(cur)
@@ -255,7 +255,7 @@ class LearnedOptionCollector:
             buf.termination_options[t].copy_(prior)
             buf.termination_valid[t].copy_(~force_new)
             beta_logits = self.actor.selected_termination_logits(termination_logits, prior.reshape(-1))
-            terminate = self.sample_termination(Bernoulli(logits=beta_logits)).bool().view(E, N)
+            terminate = self.sample_termination(Bernoulli(validate_args=False, logits=beta_logits)).bool().view(E, N)
             switch = terminate | force_new
             torch.where(switch, proposed, cur, out=cur)
             buf.options[t].copy_(cur)

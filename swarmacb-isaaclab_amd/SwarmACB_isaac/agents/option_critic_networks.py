@@ -39,11 +39,13 @@ class FixedOptionManager(nn.Module):
         z = torch.zeros(1, batch_size, self.hidden_size, device=device)
         return z, z.clone()
 
-    def forward_sequence(self, obs_seq: torch.Tensor, state=None):
-        """(B, T, obs) -> selector logits (B, T, O), termination logits (B, T, O), memory."""
+    def forward_sequence(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
+        """(B, T, obs) -> selector logits (B, T, O), termination logits (B, T, O), memory.
+        keep (B, T): the memory is multiplied by keep[:, t] after step t."""
         B, T = obs_seq.shape[:2]
         enc = self.encoder(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
-        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device))
+        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device),
+                         keep)
         return self.option_head(out), self.termination_head(out), nxt
 
     def step(self, obs: torch.Tensor, state=None):
@@ -51,7 +53,7 @@ class FixedOptionManager(nn.Module):
         return opt[:, 0], term[:, 0], nxt
 
     def get_option_dist(self, option_logits: torch.Tensor) -> Categorical:
-        return Categorical(logits=option_logits)
+        return Categorical(validate_args=False, logits=option_logits)
 
     def get_termination_dist(self, termination_logits: torch.Tensor, options: torch.Tensor) -> Bernoulli:
-        return Bernoulli(logits=termination_logits.gather(-1, options.long().unsqueeze(-1)).squeeze(-1))
+        return Bernoulli(validate_args=False, logits=termination_logits.gather(-1, options.long().unsqueeze(-1)).squeeze(-1))

@@ -113,18 +113,12 @@ class FixedOptionCriticTrainer(TrainerBase):
 
     # ------------------------------------------------------------ losses
     def _manager_sequence(self, batch: dict):
-        """Masked per-step LSTM unroll of the manager (OCT:492-509)."""
-        obs, dones = batch["obs"], batch["dones"]
-        B, L = obs.shape[:2]
+        """Selector logits of the manager over the minibatch sequences with the memory of
+        rows whose episode ended at t zeroed before step t+1 (the per-step loop of
+        OCT:492-509, as one masked sequence)."""
         state = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
-        logits = []
-        for t in range(L):
-            opt_t, _term_t, state = self.manager.step(obs[:, t], state)
-            logits.append(opt_t)
-            if t < L - 1:
-                keep = (1.0 - dones[:, t]).view(1, B, 1)
-                state = (state[0] * keep, state[1] * keep)
-        return torch.stack(logits, dim=1)
+        option_logits, _term, _ = self.manager.forward_sequence(batch["obs"], state, keep=1.0 - batch["dones"])
+        return option_logits
 
     def _compute_sequence_losses(self, batch: dict, current_eps: float):
         """option_critic_trainer.py:459-666: (policy, value, joint option value, baseline,
@@ -137,7 +131,7 @@ class FixedOptionCriticTrainer(TrainerBase):
         N = critic_states.shape[2]
 
         option_logits = self._manager_sequence(batch)
-        opt_dist = Categorical(logits=option_logits.reshape(B * L, O))
+        opt_dist = Categorical(validate_args=False, logits=option_logits.reshape(B * L, O))
         new_logp = opt_dist.log_prob(options.reshape(-1)).view(B, L)
         ent = opt_dist.entropy().view(B, L)
         # PPO clip over the switch decisions (option_mask) inside the loss mask (OCT:515-525)
@@ -200,7 +194,7 @@ class FixedOptionCriticTrainer(TrainerBase):
             option_advantage = (next_q - reselection).reshape(B, L)
         term_signal = option_advantage + self.cfg.termination_penalty
         termination_loss = (next_beta * term_signal * term_mask).sum() / n_term
-        termination_entropy = (Bernoulli(logits=next_beta_logits).entropy() * term_mask).sum() / n_term
+        termination_entropy = (Bernoulli(validate_args=False, logits=next_beta_logits).entropy() * term_mask).sum() / n_term
         mean_beta = (next_beta * term_mask).sum().detach() / n_term
         mean_option_advantage = (option_advantage * term_mask).sum() / n_term
         return (policy_loss, value_loss, joint_loss, baseline_loss, termination_loss, option_entropy,

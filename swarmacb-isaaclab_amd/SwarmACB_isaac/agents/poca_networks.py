@@ -71,15 +71,98 @@ def _mlagents_lstm(input_size: int, memory_size: int, forget_bias: float = 1.0) 
 FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of the reference path)
 
 
-def _lstm(lstm: nn.LSTM, seq: torch.Tensor, state):
-    """lstm(seq, state) for a batch-first single-layer nn.LSTM. Rollout-time calls
-    (one step, no autograd, on the GPU) take the fused path: the gate
-    pre-activations as two library GEMMs, then swarm_lstm_cell (include/swarmcritic.h)
-    for the cell update; everything else runs torch's LSTM."""
+def _plain_lstm(lstm: nn.LSTM) -> bool:
+    return (lstm.num_layers == 1 and not lstm.bidirectional and lstm.batch_first and lstm.proj_size == 0
+            and lstm.bias)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _LSTMSequence(torch.autograd.Function):
+    """Whole-sequence LSTM recurrence on swarm_lstm_seq_forward / _backward
+    (include/swarmtrain.h): inputs are the gate pre-activations xg = x W_ih^T + b_ih
+    + b_hh (n, T, 4U), W_hh, the initial state and the optional per-step state mask;
+    outputs the hidden sequence (n, T, U) and the final cell state (n, U)."""
+
+    @staticmethod
+    def forward(ctx, xg, w_hh, h0, c0, keep):
+        n, T, G = xg.shape
+        U = G // 4
+        h_out = torch.empty(n, T, U, dtype=xg.dtype, device=xg.device)
+        c_out = torch.empty_like(h_out)
+        act = torch.empty_like(xg)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(xg.device).cuda_stream)
+        _native.check(lib.swarm_lstm_seq_forward(n, T, U, _ptr(xg), _ptr(w_hh), _ptr(h0), _ptr(c0), _ptr(keep),
+                                                 _ptr(h_out), _ptr(c_out), _ptr(act), stream),
+                      "swarm_lstm_seq_forward")
+        ctx.save_for_backward(w_hh, h0, c0, keep, h_out, c_out, act)
+        return h_out, c_out[:, -1].contiguous()
+
+    @staticmethod
+    def backward(ctx, dh_out, dc_n):
+        w_hh, h0, c0, keep, h_out, c_out, act = ctx.saved_tensors
+        n, T, U = h_out.shape
+        dxg = torch.empty_like(act)
+        dh0 = torch.empty_like(h0)
+        dc0 = torch.empty_like(c0)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(act.device).cuda_stream)
+        _native.check(lib.swarm_lstm_seq_backward(n, T, U, _ptr(w_hh), _ptr(c0), _ptr(keep), _ptr(c_out), _ptr(act),
+                                                  _ptr(dh_out.contiguous()), None, _ptr(dc_n.contiguous()),
+                                                  _ptr(dxg), _ptr(dh0), _ptr(dc0), stream),
+                      "swarm_lstm_seq_backward")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            # W_hh's gradient: dgates^T h_prev' over every (sequence, step) row, one GEMM
+            prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
+            h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
+            dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
+        return dxg, dw, dh0, dc0, None
+
+
+def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
+    """lstm(seq, state) for a batch-first single-layer nn.LSTM, optionally with the
+    carried state masked between steps: keep (n, T) multiplies (h, c) after step t
+    before step t + 1 — the trainers' per-step loops that zero the memory of rows
+    whose episode ended (poca_trainer.py:706-723, option_critic_trainer.py:496-506).
+    On the GPU the recurrence is one swarm_lstm_seq_* launch each way (autograd
+    supported); elsewhere the reference's loop of nn.LSTM calls."""
     n, T, _ = seq.shape
-    if not (FUSED_LSTM and T == 1 and seq.is_cuda and not torch.is_grad_enabled() and lstm.num_layers == 1
-            and not lstm.bidirectional and lstm.batch_first and lstm.proj_size == 0 and lstm.bias):
+    units = lstm.hidden_size
+    if (FUSED_LSTM and seq.is_cuda and _plain_lstm(lstm) and units <= _native.LSTM_SEQ_MAX_UNITS
+            and seq.dtype == torch.float32):
+        xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
+        h0 = state[0].reshape(n, units).contiguous()
+        c0 = state[1].reshape(n, units).contiguous()
+        k = keep.to(torch.float32).contiguous() if keep is not None else None
+        out, c_n = _LSTMSequence.apply(xg.contiguous(), lstm.weight_hh_l0.contiguous(), h0, c0, k)
+        return out, (out[:, -1].unsqueeze(0), c_n.unsqueeze(0))
+    if keep is None:
         return lstm(seq, state)
+    outs = []
+    for t in range(T):
+        o, state = lstm(seq[:, t:t + 1], state)
+        outs.append(o)
+        if t < T - 1:
+            k = keep[:, t].reshape(1, n, 1).to(o.dtype)
+            state = (state[0] * k, state[1] * k)
+    return torch.cat(outs, dim=1), state
+
+
+def _lstm(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
+    """lstm(seq, state) for a batch-first single-layer nn.LSTM. Rollout-time calls
+    (one step, no autograd, on the GPU) take the fused cell path: the gate
+    pre-activations as two library GEMMs, then swarm_lstm_cell
+    (include/swarmcritic.h) for the cell update. Every other GPU call (the
+    updates' sequences, with autograd) goes through lstm_sequence's
+    whole-sequence kernels."""
+    n, T, _ = seq.shape
+    if not (FUSED_LSTM and T == 1 and keep is None and seq.is_cuda and not torch.is_grad_enabled()
+            and _plain_lstm(lstm)):
+        return lstm_sequence(lstm, seq, state, keep)
     units = lstm.hidden_size
     h0, c0 = state
     h0 = h0.reshape(n, units)
@@ -150,7 +233,7 @@ class Actor(nn.Module):
         return mu, (mu * 0 + self.log_std).exp()
 
     def get_dist(self, obs: torch.Tensor) -> Normal:
-        return Normal(*self(obs))
+        return Normal(*self(obs), validate_args=False)
 
     def evaluate(self, obs: torch.Tensor, actions: torch.Tensor):
         dist = self.get_dist(obs)
@@ -170,7 +253,7 @@ class DiscreteActor(nn.Module):
         return self.logits_head(self.net(obs))
 
     def get_dist(self, obs: torch.Tensor) -> torch.distributions.Categorical:
-        return torch.distributions.Categorical(logits=self(obs))
+        return torch.distributions.Categorical(validate_args=False, logits=self(obs))
 
     def evaluate(self, obs: torch.Tensor, actions: torch.Tensor):
         dist = self.get_dist(obs)
@@ -193,10 +276,13 @@ class RecurrentDiscreteActor(nn.Module):
         z = torch.zeros(1, batch_size, self.hidden_size, device=device)
         return z, z.clone()
 
-    def forward_sequence(self, obs_seq: torch.Tensor, state=None):
+    def forward_sequence(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
+        """(B, T, obs) -> logits (B, T, A), memory. keep (B, T): the memory is multiplied by
+        keep[:, t] after step t (the trainer's per-step episode-end resets)."""
         B, T = obs_seq.shape[:2]
         enc = self.net(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
-        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device))
+        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device),
+                         keep)
         return self.logits_head(out), nxt
 
     def step(self, obs: torch.Tensor, state=None):
@@ -207,12 +293,12 @@ class RecurrentDiscreteActor(nn.Module):
         return self.step(obs)[0]
 
     def get_dist(self, obs: torch.Tensor, state=None) -> torch.distributions.Categorical:
-        return torch.distributions.Categorical(logits=self.step(obs, state)[0])
+        return torch.distributions.Categorical(validate_args=False, logits=self.step(obs, state)[0])
 
     def evaluate_sequence(self, obs_seq: torch.Tensor, actions_seq: torch.Tensor, state=None):
         B, T = obs_seq.shape[:2]
         logits, _ = self.forward_sequence(obs_seq, state)
-        dist = torch.distributions.Categorical(logits=logits.reshape(B * T, self.num_actions))
+        dist = torch.distributions.Categorical(validate_args=False, logits=logits.reshape(B * T, self.num_actions))
         act = actions_seq.reshape(B * T, -1).squeeze(-1).long()
         return dist.log_prob(act).view(B, T, 1), dist.entropy().view(B, T)
 

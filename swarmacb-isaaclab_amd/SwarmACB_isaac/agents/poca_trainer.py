@@ -138,21 +138,16 @@ class POCATrainer(TrainerBase):
         return policy_loss, value_loss, baseline_loss, mean_entropy
 
     def _actor_sequence(self, batch: dict):
-        """Per-step masked LSTM unroll of the recurrent actor (PT:706-723): memories of
-        rows whose episode ended at t are zeroed before step t+1."""
+        """The recurrent actor over the minibatch sequences with the memory of rows whose
+        episode ended at t zeroed before step t+1 (the per-step loop of PT:706-723, as one
+        masked sequence: one swarm_lstm_seq launch each way on the GPU)."""
         obs, actions = batch["obs"], batch["actions"]
         B, L = obs.shape[:2]
         state = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
-        logps, ents = [], []
-        for t in range(L):
-            logits, state = self.actor.step(obs[:, t], state)
-            dist = torch.distributions.Categorical(logits=logits)
-            logps.append(dist.log_prob(actions[:, t].squeeze(-1).long()).unsqueeze(-1))
-            ents.append(dist.entropy())
-            if t < L - 1:
-                keep = (1.0 - batch["dones"][:, t]).view(1, B, 1)
-                state = (state[0] * keep, state[1] * keep)
-        return torch.stack(logps, dim=1), torch.stack(ents, dim=1)
+        logits, _ = self.actor.forward_sequence(obs, state, keep=1.0 - batch["dones"])
+        dist = torch.distributions.Categorical(validate_args=False, logits=logits.reshape(B * L, -1))
+        logp = dist.log_prob(actions.reshape(B * L).long()).view(B, L, 1)
+        return logp, dist.entropy().view(B, L)
 
     def _compute_recurrent_losses(self, batch: dict, current_eps: float):
         """poca_trainer.py:690-775."""

@@ -1,0 +1,183 @@
+// swarm_lstm.hip — whole-sequence LSTM recurrence for the trainers' PPO updates
+// (declared in include/swarmtrain.h).
+//
+// One 256-thread workgroup per sequence walks all T steps: the forward keeps
+// its gate row of W_hh in registers (thread j = gate pre-activation j, up to
+// 4 x 64 units) and the carried (masked) h in LDS, so a step is one register dot
+// product, one activation, one cell update and two barriers; the backward keeps
+// the W_hh^T slice it needs in registers and walks the steps in reverse. A
+// minibatch of the ML-Agents trainers (16 sequences x 128 steps) is then one
+// launch instead of 128 library LSTM calls (forward) plus 128 (backward).
+// Precise expf / tanhf: the results match torch.nn.LSTM to fp32 rounding.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/swarmstep.h"
+#include "../../include/swarmtrain.h"
+#include "swarm_launch.h"
+
+namespace {
+
+constexpr int MAXU = 64;    // units per LSTM (4 x 64 gate rows = the 256 threads)
+constexpr int NT = 256;
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const float* __restrict__ xg,
+                                                          const float* __restrict__ w_hh,
+                                                          const float* __restrict__ h0,
+                                                          const float* __restrict__ c0,
+                                                          const float* __restrict__ keep, float* __restrict__ h_out,
+                                                          float* __restrict__ c_out, float* __restrict__ act) {
+    __shared__ float hs[MAXU];
+    __shared__ float gs[4 * MAXU];
+    const int64_t b = blockIdx.x;
+    const int j = threadIdx.x;
+    const int G = 4 * U;
+    float w[MAXU];
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) w[k] = (j < G && k < U) ? w_hh[j * U + k] : 0.0f;
+    float c = 0.0f;
+    if (j < U) {
+        hs[j] = h0[b * U + j];
+        c = c0[b * U + j];
+    }
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+        const int64_t row = b * T + t;
+        if (j < G) {
+            float a = 0.0f;
+#pragma unroll
+            for (int k = 0; k < MAXU; ++k)
+                if (k < U) a += w[k] * hs[k];
+            a += xg[row * G + j];
+            const int kind = j / U;                      // 0 i, 1 f, 2 g, 3 o
+            const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
+            gs[j] = v;
+            act[row * G + j] = v;
+        }
+        __syncthreads();
+        if (j < U) {
+            c = gs[U + j] * c + gs[j] * gs[2 * U + j];
+            const float h = gs[3 * U + j] * tanhf(c);
+            h_out[row * U + j] = h;
+            c_out[row * U + j] = c;
+            // the state carried into step t + 1 is masked where the episode ended at t
+            const float kk = (keep && t + 1 < T) ? keep[row] : 1.0f;
+            hs[j] = h * kk;
+            c *= kk;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const float* __restrict__ w_hh,
+                                                          const float* __restrict__ c0,
+                                                          const float* __restrict__ keep,
+                                                          const float* __restrict__ c_out,
+                                                          const float* __restrict__ act,
+                                                          const float* __restrict__ dh_out,
+                                                          const float* __restrict__ dh_n,
+                                                          const float* __restrict__ dc_n, float* __restrict__ dxg,
+                                                          float* __restrict__ dh0, float* __restrict__ dc0) {
+    __shared__ float dgs[4 * MAXU];
+    __shared__ float part[4 * MAXU];
+    __shared__ float dhr[MAXU];
+    const int64_t b = blockIdx.x;
+    const int j = threadIdx.x;
+    const int G = 4 * U;
+    // thread j < G sums quarter q = j / U of the gate rows for unit u = j % U:
+    // dh_prev'[u] = sum_{r} W_hh[r][u] dgates[r]
+    const int q = j / (U > 0 ? U : 1), u = j - q * U;
+    float wt[MAXU];
+#pragma unroll
+    for (int m = 0; m < MAXU; ++m) wt[m] = (j < G && m < U) ? w_hh[(q * U + m) * U + u] : 0.0f;
+    float dc_rec = 0.0f, dc_prev = 0.0f;
+    if (j < U) {
+        dhr[j] = dh_n ? dh_n[b * U + j] : 0.0f;
+        dc_rec = dc_n ? dc_n[b * U + j] : 0.0f;
+    }
+    __syncthreads();
+    for (int t = T - 1; t >= 0; --t) {
+        const int64_t row = b * T + t;
+        if (j < U) {
+            const float* a = act + row * G;
+            const float ig = a[j], fg = a[U + j], gg = a[2 * U + j], og = a[3 * U + j];
+            const float ct = c_out[row * U + j];
+            const float kprev = (t > 0 && keep) ? keep[row - 1] : 1.0f;
+            const float cp = t > 0 ? c_out[(row - 1) * U + j] * kprev : c0[b * U + j];
+            const float dh = dh_out[row * U + j] + dhr[j];
+            const float tc = tanhf(ct);
+            const float dc = dc_rec + dh * og * (1.0f - tc * tc);
+            const float gi = dc * gg * ig * (1.0f - ig);
+            const float gf = dc * cp * fg * (1.0f - fg);
+            const float gg2 = dc * ig * (1.0f - gg * gg);
+            const float go = dh * tc * og * (1.0f - og);
+            dgs[j] = gi;
+            dgs[U + j] = gf;
+            dgs[2 * U + j] = gg2;
+            dgs[3 * U + j] = go;
+            float* d = dxg + row * G;
+            d[j] = gi;
+            d[U + j] = gf;
+            d[2 * U + j] = gg2;
+            d[3 * U + j] = go;
+            dc_prev = dc * fg;
+        }
+        __syncthreads();
+        if (j < G) {
+            float s = 0.0f;
+#pragma unroll
+            for (int m = 0; m < MAXU; ++m)
+                if (m < U) s += wt[m] * dgs[q * U + m];
+            part[j] = s;
+        }
+        __syncthreads();
+        if (j < U) {
+            const float dhp = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
+            if (t > 0) {
+                const float kk = keep ? keep[row - 1] : 1.0f;
+                dhr[j] = dhp * kk;
+                dc_rec = dc_prev * kk;
+            } else {
+                if (dh0) dh0[b * U + j] = dhp;
+                if (dc0) dc0[b * U + j] = dc_prev;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+bool args_ok(int64_t n, int32_t T, int32_t units) {
+    return n >= 0 && n <= 0x7fffffff && T >= 1 && units >= 1 && units <= MAXU;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t swarm_lstm_seq_forward(int64_t n, int32_t T, int32_t units, const float* xg, const float* w_hh,
+                               const float* h0, const float* c0, const float* keep, float* h_out, float* c_out,
+                               float* act, void* stream) {
+    if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
+    if (n == 0) return SWARM_OK;
+    if (!xg || !w_hh || !h0 || !c0 || !h_out || !c_out || !act) return SWARM_ERR_ARG;
+    lstm_seq_fwd_kernel<<<(unsigned)n, NT, 0, static_cast<hipStream_t>(stream)>>>(T, units, xg, w_hh, h0, c0, keep,
+                                                                                 h_out, c_out, act);
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float* w_hh, const float* c0,
+                                const float* keep, const float* c_out, const float* act, const float* dh_out,
+                                const float* dh_n, const float* dc_n, float* dxg, float* dh0, float* dc0,
+                                void* stream) {
+    if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
+    if (n == 0) return SWARM_OK;
+    if (!w_hh || !c0 || !c_out || !act || !dh_out || !dxg) return SWARM_ERR_ARG;
+    lstm_seq_bwd_kernel<<<(unsigned)n, NT, 0, static_cast<hipStream_t>(stream)>>>(
+        T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0, dc0);
+    return swarm::record_hip_status();
+}
+
+}  // extern "C"

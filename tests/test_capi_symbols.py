@@ -13,7 +13,7 @@ from SwarmACB_isaac import _native
 from SwarmACB_isaac.engine import fsm_pack, fsm_unpack
 
 HEADERS = {"swarmstep.h": _native.EXPORTS, "swarmrollout.h": _native.ROLLOUT_EXPORTS,
-           "swarmcritic.h": _native.CRITIC_EXPORTS}
+           "swarmcritic.h": _native.CRITIC_EXPORTS, "swarmtrain.h": _native.TRAIN_EXPORTS}
 
 
 def declared_functions(header: str = "swarmstep.h") -> list[str]:

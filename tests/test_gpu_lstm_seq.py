@@ -1,0 +1,70 @@
+"""The whole-sequence LSTM kernels (swarm_lstm_seq_forward / _backward,
+include/swarmtrain.h) against torch's LSTM on the same GPU: the hidden sequence,
+the final state and every gradient (input, W_ih, W_hh, both biases, initial
+state), unmasked (one nn.LSTM call over the sequence) and masked (the trainers'
+per-step loop that zeroes the carried state after episode ends)."""
+
+import pytest
+import torch
+
+from SwarmACB_isaac.agents import poca_networks as PN
+
+pytestmark = pytest.mark.gpu
+
+TOL = dict(rtol=2e-5, atol=2e-6)
+
+
+def _case(n, T, inp, units, masked, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    lstm, _ = PN._mlagents_lstm(inp, 2 * units)
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.add_(torch.randn(p.shape, generator=g) * 0.1)
+    lstm = lstm.to(dev)
+    x = (torch.randn(n, T, inp, generator=g)).to(dev)
+    h0 = (torch.randn(1, n, units, generator=g) * 0.5).to(dev)
+    c0 = (torch.randn(1, n, units, generator=g) * 0.5).to(dev)
+    keep = (torch.rand(n, T, generator=g) > 0.2).float().to(dev) if masked else None
+    wout = torch.randn(n, T, units, generator=g).to(dev)
+    return lstm, x, h0, c0, keep, wout
+
+
+def _run(fused, lstm, x, h0, c0, keep, wout):
+    PN.FUSED_LSTM = fused
+    try:
+        xs, hs, cs = (t.clone().requires_grad_(True) for t in (x, h0, c0))
+        lstm.zero_grad()
+        out, (hn, cn) = PN.lstm_sequence(lstm, xs, (hs, cs), keep)
+        loss = (out * wout).sum() + (hn ** 2).sum() + (cn * 0.3).sum()
+        loss.backward()
+        grads = [xs.grad, hs.grad, cs.grad] + [p.grad.clone() for p in lstm.parameters()]
+        return [out.detach(), hn.detach(), cn.detach()], grads
+    finally:
+        PN.FUSED_LSTM = True
+
+
+@pytest.mark.parametrize("n,T,inp,units,masked", [(16, 128, 128, 64, True), (16, 128, 128, 64, False),
+                                                  (96, 128, 128, 64, False), (5, 7, 16, 8, True),
+                                                  (12288, 1, 128, 32, False), (3, 2, 4, 1, True)])
+def test_lstm_sequence_matches_torch(gpu_device, n, T, inp, units, masked):
+    case = _case(n, T, inp, units, masked, gpu_device)
+    outs_k, grads_k = _run(True, *case)
+    outs_t, grads_t = _run(False, *case)
+    for a, b in zip(outs_k, outs_t):
+        torch.testing.assert_close(a, b, **TOL)
+    names = ["x", "h0", "c0", "w_ih", "w_hh", "b_ih", "b_hh"]
+    for name, a, b in zip(names, grads_k, grads_t):
+        scale = max(1.0, float(b.abs().max()))
+        torch.testing.assert_close(a / scale, b / scale, rtol=1e-4, atol=1e-5, msg=name)
+
+
+def test_lstm_sequence_rejects_wide_units(gpu_device):
+    """> 64 units take torch's LSTM (the kernels keep a gate row of W_hh in registers)."""
+    from SwarmACB_isaac import _native
+
+    lib = _native.load()
+    assert lib.swarm_lstm_seq_forward(1, 1, 65, *([None] * 9)) == -1
+    case = _case(4, 3, 8, 96, True, gpu_device)
+    outs_k, _ = _run(True, *case)
+    outs_t, _ = _run(False, *case)
+    torch.testing.assert_close(outs_k[0], outs_t[0])

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Profile one config's PPO optimizer steps with torch.profiler (CPU + device
+activity), printing the top ops by device time and the kernel launch count per
+optimizer step. Usage: python tools/prof_train.py --config C3 [--steps 3]"""
+import argparse
+import itertools
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "swarmacb-isaaclab_amd"), os.path.join(ROOT, "tools")]
+import bench_train  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--decisions", type=int, default=128)
+    ap.add_argument("--envs", type=int, default=256)
+    a = ap.parse_args()
+    from SwarmACB_isaac.agents.config import make_env_cfg
+    from SwarmACB_isaac.agents.metrics import NullWriter
+    from SwarmACB_isaac.registry import make
+    from SwarmACB_isaac.train import make_trainer
+
+    yaml_name, _, _ = bench_train.CONFIGS[a.config]
+    run_name, variant, cfg, env_ov = bench_train.resolved_config(yaml_name)
+    env_ov["num_envs"] = a.envs
+    task = env_ov.pop("task")
+    env = make(task, make_env_cfg(task, variant, env_ov, cfg.trainer_type), device="cuda:0")
+    cfg.horizon, cfg.buffer_size_hint, cfg.log_dir = a.decisions, 0, "/tmp/prof_train"
+    tr = make_trainer(env, cfg)
+    tr.writer = NullWriter()
+    obs, _ = env.reset()
+    tr._on_train_start()
+    tr.collect_rollout(obs, a.decisions)
+    orig = tr._sequence_batches
+    cfg.num_epochs = 1
+    tr._sequence_batches = lambda: itertools.islice(orig(), 2)
+    tr.update()
+    torch.cuda.synchronize()
+    tr._sequence_batches = lambda: itertools.islice(orig(), a.steps)
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        tr.update()
+        torch.cuda.synchronize()
+    ka = prof.key_averages()
+    print(ka.table(sort_by="cuda_time_total", row_limit=40))
+    print(ka.table(sort_by="cpu_time_total", row_limit=25))
+    n_kernels = sum(e.count for e in ka if e.device_type == torch.autograd.DeviceType.CUDA)
+    print(f"device kernels per optimizer step: {n_kernels / a.steps:.0f}")
+
+
+if __name__ == "__main__":
+    main()
