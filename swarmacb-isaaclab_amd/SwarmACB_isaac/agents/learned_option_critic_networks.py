@@ -10,7 +10,7 @@ What is MI355X-specific:
 
 * the per-option heads (option value, wheel mean, termination: 3 x 6 small
   Linear layers the reference applies one by one, LON:473-494) run as ONE
-  batched contraction per head kind over the stacked head weights;
+  GEMM over the stacked head weights of all options;
 * at rollout time (one step, no autograd, on the GPU) both LSTMs take the
   fused path of poca_networks._lstm (gate GEMMs + the swarm_lstm_cell kernel);
   the option LSTM then runs over E·N·6 rows (491,520 at C5's 4,096 envs).
@@ -74,11 +74,20 @@ class SquashedNormal:
         return self.base_dist.entropy()
 
 
-def _head_stack(heads: nn.ModuleList, feats: torch.Tensor) -> torch.Tensor:
-    """[head_o(feats[..., o, :]) for o] as one contraction: (..., O, H) -> (..., O, out)."""
-    w = torch.stack([h.weight for h in heads])     # (O, out, H)
-    b = torch.stack([h.bias for h in heads])       # (O, out)
-    return torch.einsum("...oh,okh->...ok", feats, w) + b
+def _option_heads(head_lists, feats: torch.Tensor) -> list[torch.Tensor]:
+    """[[head_o(feats[..., o, :]) for o] for every head kind] as ONE GEMM: every option's
+    feature row meets the stacked weights of all options' heads (O x sum(out) columns,
+    a few dozen), and the diagonal option blocks are kept. (..., O, H) -> per kind
+    (..., O, out)."""
+    O, H = feats.shape[-2], feats.shape[-1]
+    outs = [hl[0].out_features for hl in head_lists]
+    K = sum(outs)
+    w = torch.cat([torch.cat([hl[o].weight for hl in head_lists], 0) for o in range(O)], 0)    # (O K, H)
+    b = torch.stack([torch.cat([hl[o].bias for hl in head_lists], 0) for o in range(O)])       # (O, K)
+    lead = feats.shape[:-2]
+    y = torch.nn.functional.linear(feats.reshape(-1, H), w).view(-1, O, O, K)
+    y = torch.diagonal(y, dim1=1, dim2=2).transpose(1, 2) + b                                # (rows, O, K)
+    return [t.reshape(*lead, O, n) for t, n in zip(torch.split(y, outs, dim=-1), outs)]
 
 
 class LearnedOptionActor(nn.Module):
@@ -228,11 +237,12 @@ class LearnedOptionActor(nn.Module):
         option_features = self.option_output_encoder(
             torch.cat([option_enc, option_rec], dim=-1).reshape(-1, H + self.option_recurrent_size)
         ).view(B, O, T, H).permute(0, 2, 1, 3)
-        option_values = _head_stack(self.option_value_heads, option_features).squeeze(-1)
-        selector_logits = (_head_stack(self.selector_heads, option_features).squeeze(-1)
-                           if self.separate_selector else option_values)
-        action_means = _head_stack(self.action_heads, option_features)
-        termination_logits = _head_stack(self.termination_heads, option_features).squeeze(-1)
+        kinds = [self.option_value_heads, self.action_heads, self.termination_heads]
+        if self.separate_selector:
+            kinds.append(self.selector_heads)
+        heads = _option_heads(kinds, option_features)
+        option_values, action_means, termination_logits = heads[0].squeeze(-1), heads[1], heads[2].squeeze(-1)
+        selector_logits = heads[3].squeeze(-1) if self.separate_selector else option_values
         action_stds = self.option_log_stds().exp().view(1, 1, O, self.act_dim).expand_as(action_means)
         next_state = self._pack_state(next_manager_state, next_option_state, B)
         return selector_logits, option_values, termination_logits, action_means, action_stds, attentions, next_state

@@ -30,7 +30,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const fl
                                                           const float* __restrict__ c0,
                                                           const float* __restrict__ keep, float* __restrict__ h_out,
                                                           float* __restrict__ c_out, float* __restrict__ act) {
-    __shared__ float hs[MAXU];
+    __shared__ __attribute__((aligned(16))) float hs[MAXU];
     __shared__ float gs[4 * MAXU];
     const int64_t b = blockIdx.x;
     const int j = threadIdx.x;
@@ -39,20 +39,30 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const fl
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) w[k] = (j < G && k < U) ? w_hh[j * U + k] : 0.0f;
     float c = 0.0f;
-    if (j < U) {
-        hs[j] = h0[b * U + j];
-        c = c0[b * U + j];
-    }
+    if (j < MAXU) hs[j] = j < U ? h0[b * U + j] : 0.0f;   // padded to a multiple of 4 for float4 reads
+    if (j < U) c = c0[b * U + j];
+    const int kind = j / (U > 0 ? U : 1);                // 0 i, 1 f, 2 g, 3 o
+    // the step's global inputs are loaded one step ahead, off the recurrence's critical path
+    float x_next = j < G ? xg[b * T * G + j] : 0.0f;
+    float k_next = (keep && j < U) ? keep[b * T] : 1.0f;
     __syncthreads();
     for (int t = 0; t < T; ++t) {
         const int64_t row = b * T + t;
+        const float x = x_next, kk = (t + 1 < T) ? k_next : 1.0f;
+        if (t + 1 < T) {
+            if (j < G) x_next = xg[(row + 1) * G + j];
+            if (keep && j < U) k_next = keep[row + 1];
+        }
         if (j < G) {
-            float a = 0.0f;
+            float a0 = 0.0f, a1 = 0.0f;
 #pragma unroll
-            for (int k = 0; k < MAXU; ++k)
-                if (k < U) a += w[k] * hs[k];
-            a += xg[row * G + j];
-            const int kind = j / U;                      // 0 i, 1 f, 2 g, 3 o
+            for (int k = 0; k < MAXU; k += 4)
+                if (k < U) {
+                    const float4 h4 = *reinterpret_cast<const float4*>(&hs[k]);
+                    a0 += w[k] * h4.x + w[k + 2] * h4.z;
+                    a1 += w[k + 1] * h4.y + w[k + 3] * h4.w;
+                }
+            const float a = (a0 + a1) + x;
             const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
             gs[j] = v;
             act[row * G + j] = v;
@@ -64,7 +74,6 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const fl
             h_out[row * U + j] = h;
             c_out[row * U + j] = c;
             // the state carried into step t + 1 is masked where the episode ended at t
-            const float kk = (keep && t + 1 < T) ? keep[row] : 1.0f;
             hs[j] = h * kk;
             c *= kk;
         }
@@ -98,22 +107,41 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const fl
         dhr[j] = dh_n ? dh_n[b * U + j] : 0.0f;
         dc_rec = dc_n ? dc_n[b * U + j] : 0.0f;
     }
+    // a step's saved activations / cells / output gradient, loaded one step ahead of use
+    struct StepIn {
+        float ig, fg, gg, og, ct, cp, kprev, dh;
+    };
+    auto load = [&](int t) {
+        StepIn v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
+        if (j < U) {
+            const int64_t row = b * T + t;
+            const float* a = act + row * G;
+            v.ig = a[j];
+            v.fg = a[U + j];
+            v.gg = a[2 * U + j];
+            v.og = a[3 * U + j];
+            v.ct = c_out[row * U + j];
+            v.kprev = (t > 0 && keep) ? keep[row - 1] : 1.0f;
+            v.cp = t > 0 ? c_out[(row - 1) * U + j] : c0[b * U + j];
+            v.dh = dh_out[row * U + j];
+        }
+        return v;
+    };
+    StepIn nxt = load(T - 1);
     __syncthreads();
     for (int t = T - 1; t >= 0; --t) {
         const int64_t row = b * T + t;
+        const StepIn in = nxt;
+        if (t > 0) nxt = load(t - 1);
         if (j < U) {
-            const float* a = act + row * G;
-            const float ig = a[j], fg = a[U + j], gg = a[2 * U + j], og = a[3 * U + j];
-            const float ct = c_out[row * U + j];
-            const float kprev = (t > 0 && keep) ? keep[row - 1] : 1.0f;
-            const float cp = t > 0 ? c_out[(row - 1) * U + j] * kprev : c0[b * U + j];
-            const float dh = dh_out[row * U + j] + dhr[j];
-            const float tc = tanhf(ct);
-            const float dc = dc_rec + dh * og * (1.0f - tc * tc);
-            const float gi = dc * gg * ig * (1.0f - ig);
-            const float gf = dc * cp * fg * (1.0f - fg);
-            const float gg2 = dc * ig * (1.0f - gg * gg);
-            const float go = dh * tc * og * (1.0f - og);
+            const float cp = t > 0 ? in.cp * in.kprev : in.cp;
+            const float dh = in.dh + dhr[j];
+            const float tc = tanhf(in.ct);
+            const float dc = dc_rec + dh * in.og * (1.0f - tc * tc);
+            const float gi = dc * in.gg * in.ig * (1.0f - in.ig);
+            const float gf = dc * cp * in.fg * (1.0f - in.fg);
+            const float gg2 = dc * in.ig * (1.0f - in.gg * in.gg);
+            const float go = dh * tc * in.og * (1.0f - in.og);
             dgs[j] = gi;
             dgs[U + j] = gf;
             dgs[2 * U + j] = gg2;
@@ -123,23 +151,25 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const fl
             d[U + j] = gf;
             d[2 * U + j] = gg2;
             d[3 * U + j] = go;
-            dc_prev = dc * fg;
+            dc_prev = dc * in.fg;
         }
         __syncthreads();
         if (j < G) {
-            float s = 0.0f;
+            float s0 = 0.0f, s1 = 0.0f;
 #pragma unroll
-            for (int m = 0; m < MAXU; ++m)
-                if (m < U) s += wt[m] * dgs[q * U + m];
-            part[j] = s;
+            for (int m = 0; m < MAXU; m += 2)
+                if (m < U) {
+                    s0 += wt[m] * dgs[q * U + m];
+                    if (m + 1 < U) s1 += wt[m + 1] * dgs[q * U + m + 1];
+                }
+            part[j] = s0 + s1;
         }
         __syncthreads();
         if (j < U) {
             const float dhp = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
             if (t > 0) {
-                const float kk = keep ? keep[row - 1] : 1.0f;
-                dhr[j] = dhp * kk;
-                dc_rec = dc_prev * kk;
+                dhr[j] = dhp * in.kprev;
+                dc_rec = dc_prev * in.kprev;
             } else {
                 if (dh0) dh0[b * U + j] = dhp;
                 if (dc0) dc0[b * U + j] = dc_prev;

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--minibatches", type=int, default=8, help="minibatches per epoch in the timed update")
     ap.add_argument("--warmup-minibatches", type=int, default=2)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--matmul-precision", default=None, help="override the config's matmul_precision (OC2)")
     args, _ = ap.parse_known_args()
     names = sorted(CONFIGS) if args.config == "all" else [args.config]
     for name in names:
@@ -94,6 +95,8 @@ def run(name, args):
     cfg.buffer_size_hint = 0
     cfg.total_timesteps = max(cfg.total_timesteps, 10 ** 9)
     cfg.log_dir = os.path.join("/tmp", "bench_train_runs", run_name)
+    if args.matmul_precision and hasattr(cfg, "matmul_precision"):
+        cfg.matmul_precision = args.matmul_precision
     tr = make_trainer(env, cfg)
     tr.writer = NullWriter()
     N, dp = env.num_agents, tr.decision_period
@@ -153,6 +156,7 @@ def run(name, args):
                              "projected_update_s": steps_ep * ms_step / 1e3,
                              "projected_rollout_s": T_ep * ms_dec / 1e3, "projected_iteration_s": iter_s,
                              "agent_steps_per_s_end_to_end": E * N * dp * T_ep / iter_s},
+        "matmul_precision": getattr(cfg, "matmul_precision", "highest"),
         "peak_mem_gb": torch.cuda.max_memory_allocated(dev) / 2 ** 30,
     }
     print(json.dumps(line), flush=True)
