@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo")
     ap.add_argument("--layout", type=int, default=0,
-                    help="kernel work layout (1/2/4 waves per 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
+                    help="kernel work layout (4 = 4 waves share 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget per leg (0 = skip)")
     ap.add_argument("--prewarm", type=float, default=1.0,
                     help="seconds of untimed step launches on a scratch engine before the warm-up "

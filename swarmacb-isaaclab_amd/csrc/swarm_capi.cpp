@@ -129,7 +129,7 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     if (p->num_envs < 1 || p->num_agents < 1 || p->num_agents > SWARM_MAX_AGENTS) return SWARM_ERR_ARG;
     if (p->obs_dim != 24 && p->obs_dim != 4) return SWARM_ERR_ARG;
     if (p->max_episode_length < 1 || p->decimation < 0 || p->env_offset < 0) return SWARM_ERR_ARG;
-    if (p->layout != 0 && p->layout != 1 && p->layout != 4 && p->layout != 103) return SWARM_ERR_ARG;
+    if (p->layout != 0 && p->layout != 4 && p->layout != 103) return SWARM_ERR_ARG;
     if ((int64_t)p->num_envs * p->num_agents * 24 >= ((int64_t)1 << 31)) return SWARM_ERR_ARG;  // 32-bit indices
     if (p->layout == 103 && 3 * p->num_agents > 64) return SWARM_ERR_ARG;
     swarm_handle_t* h = new (std::nothrow) swarm_handle_t();

@@ -1470,18 +1470,11 @@ static void launch_step_t(const Geom& g, const DevState& st, const void* act, co
             SWARM_LAUNCH_STEP(0, 103);
         return;
     }
+    // layout 4 (4 waves share floor(64/N) arenas): the fallback for N > 21 robots per
+    // arena, generic-N kernel only. (Layout 1, one lane per robot, was measured at
+    // 297.7 us vs 113.1 us for layout 103 and is no longer built)
     const int blocks = (g.E + g.apb - 1) / g.apb;
-    if (g.N == 20) {
-        if (g.layout == 4)
-            SWARM_LAUNCH_STEP(20, 4);
-        else
-            SWARM_LAUNCH_STEP(20, 1);
-    } else {
-        if (g.layout == 4)
-            SWARM_LAUNCH_STEP(0, 4);
-        else
-            SWARM_LAUNCH_STEP(0, 1);
-    }
+    SWARM_LAUNCH_STEP(0, 4);
 #undef SWARM_LAUNCH_STEP
 }
 

@@ -15,7 +15,7 @@ before, kw = O.fixture_step_inputs(fx, 0)
 state = {k[len("before_"):]: v for k, v in before.items()}
 d = kw["draws"]
 res = {}
-for layout in (1, 4, 103):
+for layout in (4, 103):
     eng = SwarmEngine(meta["mission"], meta["profile"], env.E, env.N, env.obs_dim, meta["discrete"], env.cfg.max_len,
                       1, 0, 0, dev, layout=layout)
     eng.reset()
