@@ -150,7 +150,8 @@ class DirectionalGateEnvCfg:
         if bad:
             raise NotImplementedError(
                 f"{type(self).__name__}: the HIP step embeds the reference values of {bad}; "
-                "overriding them is not supported")
+                "overriding them at run time is not supported; they are compiled into the kernel "
+                "from swarmacb-isaaclab_amd/csrc/swarm_geom_build.h (edit the constant there and rebuild)")
         if abs(self.sim.dt - 0.1) > 1e-12:
             raise NotImplementedError("sim.dt must be 0.1 (10 Hz, DGC:99-101)")
         if self.profile not in ("isaac", "standalone"):

@@ -41,6 +41,8 @@ enum RngPurpose : uint32_t {
     A(float, face_nx, 12) A(float, face_ny, 12) A(float, face_px, 12) A(float, face_py, 12)                 \
     A(float, mcf_nx, 12) A(float, mcf_ny, 12) A(float, mcf_px, 12) A(float, mcf_py, 12)                     \
     S(float, wall_clear_dg) /* r + 0.5*t + eps (DG:1050-1054) */                                             \
+    /* kernel pre-filters only: face offsets -(p.n), radii inside which no face is within reach */            \
+    A(float, face_d, 12) S(float, wall_safe_r2) S(float, ins_safe_r2)                                       \
     S(float, wall_clear_mc) /* r (MC:533) */                                                                 \
     /* internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 */                                      \
     A(float, iw_nx, 3) A(float, iw_ny, 3) A(float, iw_ax, 3) A(float, iw_ay, 3) A(float, iw_tx, 3)          \

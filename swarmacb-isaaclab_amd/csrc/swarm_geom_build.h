@@ -4,6 +4,7 @@
 // Single source of truth: the C ABI builds it per handle (kernel argument) and
 // gen_tables.cpp emits it as compile-time constants for the kernels.
 #pragma once
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -66,6 +67,17 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     const double r = 0.035;
     g.wall_clear_dg = (float)(r + 0.5 * 0.01 + 1e-4);                      // DG:1050-1054
     g.wall_clear_mc = (float)r;                                             // MC:533
+    // pre-filters of the kernel (never change a result): sd_k(p) = d_k + p.n_k >= apothem - |p|,
+    // so |p| below apothem - clearance - margin means no face is within the wall clearance
+    // (wall_safe_r2) or within the 1e-3 "strictly inside" band (ins_safe_r2)
+    double apo = 1e30;
+    for (int i = 0; i < n; ++i) {
+        g.face_d[i] = (float)(-((double)g.face_px[i] * g.face_nx[i] + (double)g.face_py[i] * g.face_ny[i]));
+        apo = std::min(apo, (double)g.face_d[i]);
+    }
+    const double rs = apo - g.wall_clear_dg - 1e-4, ri = apo - 1e-3 - 1e-4;
+    g.wall_safe_r2 = (float)(rs * rs);
+    g.ins_safe_r2 = (float)(ri * ri);
 
     // mission zones (DG:649-656, DGC:163-167; SH:24-27 / MC:322-329)
     const double corr_south = ni - 1.06, gate_south = corr_south - 0.33;

@@ -42,6 +42,19 @@
 #define SWARM_UNROLLED_CHUNKS 0
 #endif
 
+// 1: wave-uniform pre-filters skip wall faces / inside tests no lane can need
+// (results unchanged); 0: every face evaluated (reference loop shape).
+#ifndef SWARM_WALL_FILTER
+#define SWARM_WALL_FILTER 1
+#endif
+
+// 1: a part's compile-time neighbour chunk is read from LDS back to back and
+// its candidate bits are formed branch-free (one LDS wait, no exec-mask
+// bookkeeping per neighbour); 0: per-neighbour loop with a divergent exit.
+#ifndef SWARM_BRANCHFREE_CHUNKS
+#define SWARM_BRANCHFREE_CHUNKS 1
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -203,14 +216,51 @@ __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     return __popcll(m & L.amask);
 }
 
+// Candidate bits of this part's neighbour chunk j0 + jj, jj < C (compile time):
+// bit jj set iff j0 + jj < j1, j0 + jj != i and pred(dx, dy) for d = p_j - p_i.
+// All C tile entries are read first (indices stay inside the 64-entry tile;
+// entries past j1 are read but masked), then tested without branches.
+template <int C, class Pred>
+__device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, float x, float y, Pred pred) {
+    float2 p[C];
+#pragma unroll
+    for (int jj = 0; jj < C; ++jj) p[jj] = xy[L.ab + L.j0 + jj];
+    uint32_t m = 0;
+#pragma unroll
+    for (int jj = 0; jj < C; ++jj) {
+        const int j = L.j0 + jj;
+        const bool c = (j < L.j1) & (j != L.i) & pred(p[jj].x - x, p[jj].y - y);
+        m |= c ? (1u << jj) : 0u;
+    }
+    return m;
+}
+
 // ---------------------------------------------------------------------------
 //  Collisions
 // ---------------------------------------------------------------------------
 
 // DG:1048-1078 — inward push summed over all penetrated faces (Jacobi).
+// Wave-uniform pre-filters skip the faces no lane of the wave can reach: a face
+// whose exact signed distance exceeds the clearance contributes pen = 0, and a
+// +-0 term leaves the sum bitwise unchanged, so only the work changes. The
+// filters use a fused estimate of sd with a 1e-4 m margin (its error is ~1e-7).
 __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
     if (SWARM_ABLATE & 8) return;
     float tx = 0.0f, ty = 0.0f;
+#if SWARM_WALL_FILTER
+    if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const float sda = fmaf(x, g.face_nx[k], fmaf(y, g.face_ny[k], g.face_d[k]));
+            if (__any(sda < g.wall_clear_dg + 1e-4f)) {
+                const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
+                const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
+                tx += pen * g.face_nx[k];
+                ty += pen * g.face_ny[k];
+            }
+        }
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
@@ -218,6 +268,7 @@ __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
         tx += pen * g.face_nx[k];
         ty += pen * g.face_ny[k];
     }
+#endif
     x = x + tx;
     y = y + ty;
 }
@@ -271,6 +322,17 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
             const float dx = x - p[jj].x, dy = y - p[jj].y;
             const float s = dx * dx + dy * dy + 1e-8f;
             if (j < L.j1 && j != L.i && s < g.min_dist2_hi) pair_term(j, dx, dy);
+        }
+    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+        // d = p_j - p_i here; the squared distance is sign-free and bit-identical
+        uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
+            return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
+        });
+        while (cand) {
+            const int j = L.j0 + __builtin_ctz(cand);
+            cand &= cand - 1u;
+            const float2 p = S.xy[L.ab + j];
+            pair_term(j, x - p.x, y - p.y);
         }
     } else {
         unsigned long long cand = 0;
@@ -509,6 +571,29 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     // for them, so the wave loops max(near) times (usually 0-1), not once per
     // segment of the part. Max is order-free: the readings are unchanged.
     uint32_t near_mask = 0;
+#if SWARM_BRANCHFREE_CHUNKS
+    // every lane tests all faces (compile-time constants, a fused estimate of sd
+    // with a 1e-4 margin: the filter only widens) and keeps its part's share
+    constexpr uint32_t part0 = [] {
+        uint32_t m = 0;
+        for (int s = 0; s < 32; s += ly_parts(LY)) m |= 1u << s;
+        return m;
+    }();
+#pragma unroll
+    for (int s = 0; s < 12; ++s) {
+        const float sda = fmaf(x, g.face_nx[s], fmaf(y, g.face_ny[s], g.face_d[s]));
+        near_mask |= sda < g.prox_range + 1e-3f + 1e-4f ? (1u << s) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= g.nint) break;
+        const float rx = x - g.iw_ax[k], ry = y - g.iw_ay[k];
+        const float u = clampf((rx * g.iw_tx[k] + ry * g.iw_ty[k]) / g.iw_lsq[k], 0.0f, 1.0f);
+        const float dx = x - (g.iw_ax[k] + u * g.iw_tx[k]), dy = y - (g.iw_ay[k] + u * g.iw_ty[k]);
+        near_mask |= dx * dx + dy * dy < (g.prox_range + 1e-3f) * (g.prox_range + 1e-3f) ? (1u << (12 + k)) : 0u;
+    }
+    near_mask &= part0 << L.p;
+#else
     for (int s = L.p; s < g.nseg; s += ly_parts(LY)) {
         bool near;
         if (s < 12) {
@@ -523,6 +608,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         }
         if (near) near_mask |= 1u << s;
     }
+#endif
     while (near_mask) {
         const int s = __builtin_ctz(near_mask);
         near_mask &= near_mask - 1u;
@@ -564,6 +650,14 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const int j = L.j0 + jj;
             const float dx = p[jj].x - x, dy = p[jj].y - y;
             if (j < L.j1 && j != L.i && dx * dx + dy * dy <= 0.0200f) disc(dx, dy);
+        }
+    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+        uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
+        while (cand) {
+            const int j = L.j0 + __builtin_ctz(cand);
+            cand &= cand - 1u;
+            const float2 p = S.xy[L.ab + j];
+            disc(p.x - x, p.y - y);
         }
     } else {
         unsigned long long cand = 0;
@@ -713,6 +807,28 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
                 uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
             }
             if (cnd[jj] && uu >= g.rab_loss) term(j, p[jj].x - x, p[jj].y - y);
+        }
+    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18) {
+        // as the K18 path below: every candidate's packet-loss uniform first (one
+        // Philox block per chunk), then the term for the kept neighbours in increasing j
+        const uint32_t cand = chunk_mask<C>(L, xy, x, y, [&](float dx, float dy) {
+            return dx * dx + dy * dy + 1e-8f < g.rab_range2_hi;
+        });
+        uint32_t kept = 0;
+        if (cand) {
+            const uint4 rb = u_replay ? make_uint4(0, 0, 0, 0)
+                                      : rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), purpose, tick);
+#pragma unroll
+            for (int jj = 0; jj < C; ++jj) {
+                const float uu = u_replay ? u_replay[min(L.j0 + jj, L.N - 1)] : u01_of7(rb, jj);
+                kept |= (((cand >> jj) & 1u) && uu >= g.rab_loss) ? (1u << jj) : 0u;
+            }
+        }
+        while (kept) {
+            const int j = L.j0 + __builtin_ctz(kept);
+            kept &= kept - 1u;
+            const float2 q = xy[L.ab + j];
+            term(j, q.x - x, q.y - y);
         }
     } else {
         unsigned long long cand = 0;
@@ -913,9 +1029,20 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 template <int LY>
 __device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y) {
     bool ins = true;
+#if SWARM_WALL_FILTER
+    // |p| < apothem - 1e-3 - margin implies every face is > 1e-3 away; the flag
+    // only selects a shortcut (a robot flagged "not inside" gets the full,
+    // exact line-of-sight test), so the conservative radius keeps results exact
+    if (__any(fmaf(x, x, y * y) >= g.ins_safe_r2)) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+            ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 12; ++k)
         ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
+#endif
     if (L.p == 0) {
         S.xy[L.r] = make_float2(x, y);
         S.ins[L.r] = ins ? 1 : 0;
