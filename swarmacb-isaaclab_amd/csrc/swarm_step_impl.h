@@ -55,6 +55,12 @@
 #define SWARM_BRANCHFREE_CHUNKS 1
 #endif
 
+// 1: the contact solver skips the partial-sum exchange when no lane of a wave
+// met a candidate pair, and stops iterating at a fixed point (results unchanged)
+#ifndef SWARM_SOLVE_SHORTCUTS
+#define SWARM_SOLVE_SHORTCUTS 1
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -302,13 +308,16 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
         if (!(ov > 0.0f)) return;
         const float inv = frcp(dist + 1e-8f);
         const float nx = dx * inv, ny = dy * inv;
-        if (j > L.i) {  // row term of pair (i, j)
-            rx += ov * nx * 0.5f;
-            ry += ov * ny * 0.5f;
-        } else {        // column term of pair (j, i): n_ji = -n_ij
-            cx += ov * (-nx) * 0.5f;
-            cy += ov * (-ny) * 0.5f;
-        }
+        // row term of pair (i, j) if j > i, else the column term of pair (j, i)
+        // (n_ji = -n_ij: ov * (-nx) * 0.5 = -(ov * nx * 0.5) exactly). Selected,
+        // not branched: the other sums add +0, which leaves them unchanged (a sum
+        // that starts at +0 never becomes -0 under round-to-nearest).
+        const float hx = ov * nx * 0.5f, hy = ov * ny * 0.5f;
+        const bool row = j > L.i;
+        rx += row ? hx : 0.0f;
+        ry += row ? hy : 0.0f;
+        cx += row ? 0.0f : -hx;
+        cy += row ? 0.0f : -hy;
     };
     if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
         // compile-time chunk: the C neighbour positions stay in registers and the
@@ -353,6 +362,15 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
         }
     }
     if constexpr (ly_parts(LY) > 1) {
+        if constexpr (ly_waves(LY) == 1 && SWARM_SOLVE_SHORTCUTS) {
+            // no lane of the wave met a candidate: every partial is +0, and
+            // (x + 0) - 0 is what the exchange below would produce
+            if (!__any(rx != 0.0f || ry != 0.0f || cx != 0.0f || cy != 0.0f)) {
+                x = (x + 0.0f) - 0.0f;
+                y = (y + 0.0f) - 0.0f;
+                return;
+            }
+        }
         S.red[0][L.tid] = make_float4(rx, ry, cx, cy);
         sync_wg<LY>();
         float4 a = S.red[0][L.pbase];
@@ -504,8 +522,10 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     }
     gate_walls<MISSION, ISAAC>(g, x, y);
     constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
+    bool fixed = false;                                   // wave-uniform
 #pragma unroll
     for (int it = 0; it <= K; ++it) {
+        if (fixed && it < K) continue;
         const float bx = x, by = y;
         if (it < K) robots_push<LY, C>(g, L, S, x, y);
         walls_dg(g, x, y);
@@ -520,6 +540,19 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
             }
         }
         gate_walls<MISSION, ISAAC>(g, x, y);
+        if constexpr (ly_waves(LY) == 1 && SWARM_SOLVE_SHORTCUTS) {
+            // Fixed point: if no robot of the wave's arenas moved in a middle
+            // iteration, every later middle iteration (same body) maps the same
+            // positions to themselves. Without internal walls the last iteration
+            // (no push) is a no-op too; with internal walls it uses the pre-step
+            // positions (and apply's first iteration does as well), so only the
+            // middle ones are skipped.
+            constexpr bool middle_from0 = !INTERNAL || !apply;
+            if ((middle_from0 ? it < K : (it >= 1 && it < K)) && !__any(x != bx || y != by)) {
+                if constexpr (!INTERNAL) return;
+                fixed = true;
+            }
+        }
     }
 }
 
