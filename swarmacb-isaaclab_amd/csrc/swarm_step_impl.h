@@ -84,8 +84,10 @@ namespace swarm {
 __device__ __forceinline__ uint4 philox4x32(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of a lo and a hi multiply
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+        const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
         c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -655,7 +657,8 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float inv = frcp(dd);
             const float t = (qx * sy - qy * sx) * inv;
             const float u = (qx * rdy[k] - qy * rdx[k]) * inv;
-            const bool hit = valid && t >= 0.0f && t <= g.prox_range && u >= 0.0f && u <= 1.0f;
+            // & (not &&): every operand is computed anyway, so the test is selects, not branches
+            const bool hit = valid & (t >= 0.0f) & (t <= g.prox_range) & (u >= 0.0f) & (u <= 1.0f);
             const float nr = hit ? 1.0f - t * g.inv_prox_range : 0.0f;
             prox[k] = fmaxf(prox[k], nr);
         }
@@ -669,7 +672,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float csq = dsq - proj * proj;
             const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
             const float hd = fmaxf(proj - hc, 0.0f);
-            const bool hit = proj > 0.0f && csq <= g.r2 && hd <= g.prox_range;
+            const bool hit = (proj > 0.0f) & (csq <= g.r2) & (hd <= g.prox_range);
             const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
