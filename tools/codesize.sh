@@ -2,7 +2,7 @@
 # Instruction count + registers of the Homing step kernels (device asm), no GPU needed.
 # EXTRA=<flags> for a variant; LAYOUT=<n> restricts to one layout (default: all).
 cd "$(dirname "$0")/../swarmacb-isaaclab_amd/csrc"
-/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -DSWARM_MISSION_ID=${MISSION:-2} $EXTRA \
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off ${STEPFLAGS--fno-slp-vectorize} -DSWARM_MISSION_ID=${MISSION:-2} $EXTRA \
   -I../../build/obj/gen --cuda-device-only -S -o /tmp/cs.s swarm_mission.hip -Rpass-analysis=kernel-resource-usage 2> /tmp/cs_res.txt || exit 1
 LAYOUT=${LAYOUT:-} python3 - <<'PY'
 import os, re
