@@ -21,6 +21,8 @@
 //            VGPRs as B fragments for the whole persistent kernel), bias +
 //            residual, LayerNorm and the mean over the set, written as pooled.
 // One persistent workgroup per CU (8 waves, two per SIMD, ~149 KiB of LDS) walks the envs.
+// BASELINES calls at N = 20 take rsa_baselines_kernel instead, which folds fc_out
+// into per-env projected value rows shared by the N sets (see there).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,6 +34,18 @@
 // design): 1 logits, 2 softmax, 4 P.V, 8 fc_out MFMA, 16 LayerNorm + pooling.
 #ifndef RSA_ABLATE
 #define RSA_ABLATE 0
+#endif
+
+// 1: BASELINES calls at N = 20 run rsa_baselines_kernel (shared projected value
+// rows); 0: rsa_pool_kernel for every mode.
+#ifndef RSA_SHARED_VW
+#define RSA_SHARED_VW 1
+#endif
+#ifndef RSA_P_WIDE
+#define RSA_P_WIDE 1
+#endif
+#ifndef RSA_GEMM_SCHED_BARRIER
+#define RSA_GEMM_SCHED_BARRIER 1
 #endif
 
 namespace {
@@ -305,6 +319,296 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
     }
 }
 
+// BASELINES mode for the reference's N = 20 (all_baselines, the dominant call):
+// fc_out is linear, so for every set row
+//   fc_out(concat_h P_h V_h) = sum_h P_h (V_h W_o,h^T) + b_o,
+// and VW_h = V_h W_o,h^T is a property of the env's entity rows, shared by all
+// N sets. Each head's projected rows are computed once per env (40 x 128 per
+// head on the matrix cores), after which the N sets' fc_out outputs are ONE
+// (N*N) x N x 128 product per head over the action rows they share; the state
+// row of set s (its own member 0) adds a rank-1 term on the VALU. That replaces
+// the per-set P.V and the (N*N) x 128 x 128 fc_out: 5056 instead of 8288
+// 16x16x4 MFMAs per env at 4 heads. The 400 x 128 outputs of an env stay in
+// VGPRs (25 row tiles of 16 per wave, each wave one 16-column tile) across the
+// heads; bias, residual, LayerNorm and the set means then run per group of 4
+// sets through LDS as in rsa_pool_kernel. Summation order differs from the
+// reference's (fp32 reassociation, ~1e-6 relative).
+template <int NH>
+__global__ void __launch_bounds__(NT) rsa_baselines_kernel(int B, const float* __restrict__ X,
+                                                            const float* __restrict__ QKV,
+                                                            const float* __restrict__ Wo,
+                                                            const float* __restrict__ bo, float* __restrict__ pooled) {
+    constexpr int N = NMAX;                 // 20 entities per set, 20 sets per env
+    constexpr int R = 2 * N;                // entity rows per env
+    constexpr int DH = HD / NH;
+    constexpr int ROWS = N * N;             // set rows per env
+    constexpr int TILES = ROWS / 16;        // 25 row tiles of 16
+#if RSA_P_WIDE
+    // P row: lane group kq's five k-steps (actions 5 kq .. 5 kq + 4) at 8 kq, so a lane reads
+    // them as one b128 + one b32; stride 36: the b128 reads of 16 lanes cover 64 banks
+    constexpr int PS = 36;
+    constexpr int PG = 8;
+#else
+    constexpr int PS = N;                   // P row stride: rows 16 B aligned; the A-fragment reads
+                                            // (20 cl + 5 kq) hit 64 distinct banks
+    constexpr int PG = N / 4;
+#endif
+    constexpr int SH = R * SW + 4;          // logit plane stride (16 B aligned rows for float4 reads)
+    constexpr int GROUPS = N / SETS;        // 5 groups of 4 sets in the epilogue
+    static_assert(ROWS % 16 == 0 && N % 4 == 0 && N % SETS == 0, "N = 20 layout");
+
+    __shared__ __attribute__((aligned(16))) float Xs[R * LDSW];
+    __shared__ __attribute__((aligned(16))) float Vs[R * LDSW];
+    __shared__ __attribute__((aligned(16))) float S[NH * SH];
+    // union: Q | K rows (logits), then one head's VW rows + P + P0, then the epilogue rows + stats
+    constexpr int U_QK = 2 * R * LDSW;
+    constexpr int U_HEAD = R * LDSW + ROWS * PS + ROWS;
+    constexpr int U_EPI = SETS * N * LDSW + SETS * 2 * N;
+    constexpr int U = U_QK > U_HEAD ? (U_QK > U_EPI ? U_QK : U_EPI) : (U_HEAD > U_EPI ? U_HEAD : U_EPI);
+    __shared__ __attribute__((aligned(16))) float Us[U];
+    float* Qs = Us;
+    float* Ks = Us + R * LDSW;
+    float* VW = Us;                          // [R][LDSW]: this head's V_h W_o,h^T rows
+    float* P = Us + R * LDSW;                // [ROWS][PS]: P[set row][action j] (0 at j = s)
+    float* P0 = P + ROWS * PS;               // [ROWS]: weight of the set's own state row
+    float* PF = Us;                          // [SETS * N][LDSW]: epilogue rows of a group
+    float* stats = Us + SETS * N * LDSW;     // [SETS][2N]
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int w = tid >> 6;                  // wave: owns output columns 16w .. 16w + 15
+    const int cl = lane & 15, kq = lane >> 4;
+    const int col = 16 * w + cl;
+
+    const float bias = bo[col];
+    const float sqrt_d = 11.313708498984761f;
+
+    for (int e = blockIdx.x; e < B; e += gridDim.x) {
+        // An opaque zero per env: row and member indices derived from it are recomputed
+        // in the loop instead of being hoisted as hundreds of loop-invariant registers
+        // (which spill next to the 100 accumulator registers).
+        int z;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        // ---- phase 0: x, q, k, v of the env's 2N entity rows
+        const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)e * R * HD);
+        const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)e * R * 3 * HD);
+        for (int i = tid; i < R * (HD / 4); i += NT) {
+            const int r = i / (HD / 4), c4 = i % (HD / 4);
+            *reinterpret_cast<float4*>(&Xs[r * LDSW + 4 * c4]) = x4[i];
+        }
+        for (int i = tid; i < R * (3 * HD / 4); i += NT) {
+            const int r = i / (3 * HD / 4), c4 = i % (3 * HD / 4), c = 4 * c4;
+            float* dst = c < HD ? &Qs[r * LDSW + c] : c < 2 * HD ? &Ks[r * LDSW + c - HD] : &Vs[r * LDSW + c - 2 * HD];
+            *reinterpret_cast<float4*>(dst) = q4[i];
+        }
+        __syncthreads();
+        // ---- phase 1: logits of every entity pair and head (as rsa_pool_kernel)
+        {
+            constexpr int TI = (R + 15) / 16;
+            constexpr int KS = DH / 4;
+            const int rl = lane & 15;
+            for (int t = w; t < NH * TI * TI; t += NT / 64) {
+                const int h = t / (TI * TI), ti = (t / TI) % TI, tj = t % TI;
+                const float* qp = &Qs[min(16 * ti + rl, R - 1) * LDSW + h * DH + KS * kq];
+                const float* kp = &Ks[min(16 * tj + rl, R - 1) * LDSW + h * DH + KS * kq];
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < KS; m += 4) {
+                    const float4 a = *reinterpret_cast<const float4*>(qp + m);
+                    const float4 bk = *reinterpret_cast<const float4*>(kp + m);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bk.x, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bk.y, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bk.z, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bk.w, acc, 0, 0, 0);
+                }
+                const int kr = 16 * tj + rl;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int qr = 16 * ti + 4 * kq + i;
+                    if (qr < R && kr < R) S[h * SH + qr * SW + kr] = acc[i] / sqrt_d;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- heads: project V_h through W_o,h, softmax of every set row, accumulate
+        f32x4 acc[TILES];
+#pragma unroll
+        for (int t = 0; t < TILES; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // softmax of set row t = (s, r) of head h over the set's members, scattered by
+        // entity: P[t][j] = weight of action row N + j (0 for j = s), P0[t] = state row s
+        auto softmax = [&](int h) {
+            if (tid < ROWS && !(RSA_ABLATE & 2)) {
+                // set s = the row's set, query = its member r; the keys of set s are the state
+                // row s (member 0) and the action rows N + j, j != s (members 1.., in j order):
+                // one scalar and five float4 reads of the query's logit row
+                const int s_ = (tid + z) / N, r = tid + z - s_ * N;
+                const float* srow = &S[h * SH + member(SWARM_RSA_BASELINES, N, s_, r) * SW];
+                float la[N];
+#pragma unroll
+                for (int c = 0; c < N / 4; ++c) {
+                    const float4 v = *reinterpret_cast<const float4*>(srow + N + 4 * c);
+                    la[4 * c] = v.x;
+                    la[4 * c + 1] = v.y;
+                    la[4 * c + 2] = v.z;
+                    la[4 * c + 3] = v.w;
+                }
+                const float ls = srow[s_];
+                float m = ls;
+#pragma unroll
+                for (int jj = 0; jj < N; ++jj) m = jj == s_ ? m : fmaxf(m, la[jj]);
+                const float es = __expf(ls - m);
+                float sum = es;   // member order: the state key, then the action keys by j
+#pragma unroll
+                for (int jj = 0; jj < N; ++jj) {
+                    la[jj] = jj == s_ ? 0.0f : __expf(la[jj] - m);
+                    sum += la[jj];
+                }
+                const float inv = 1.0f / sum;
+#if RSA_P_WIDE
+                float* prow = &P[tid * PS];
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    *reinterpret_cast<float4*>(prow + PG * g4) =
+                        make_float4(la[5 * g4] * inv, la[5 * g4 + 1] * inv, la[5 * g4 + 2] * inv, la[5 * g4 + 3] * inv);
+                    prow[PG * g4 + 4] = la[5 * g4 + 4] * inv;
+                }
+#else
+                float4* prow = reinterpret_cast<float4*>(&P[tid * PS]);
+#pragma unroll
+                for (int c = 0; c < N / 4; ++c)
+                    prow[c] = make_float4(la[4 * c] * inv, la[4 * c + 1] * inv, la[4 * c + 2] * inv, la[4 * c + 3] * inv);
+#endif
+                P0[tid] = es * inv;
+            }
+        };
+#pragma unroll 1
+        for (int h = 0; h < NH; ++h) {
+            // W_o fragments of this head for this wave's 16 columns: k-step ks of lane group
+            // kq is input feature h*DH + (DH/4) kq + ks (contiguous float4 A reads of V)
+            float wb[DH / 4];
+#pragma unroll
+            for (int ks = 0; ks < DH / 4; ++ks) wb[ks] = Wo[col * HD + h * DH + (DH / 4) * kq + ks];
+            // VW_h[row][col] for the 2N rows (3 row tiles, rows >= 2N dropped)
+#pragma unroll
+            for (int rt = 0; rt < ((RSA_ABLATE & 8) ? 0 : (R + 15) / 16); ++rt) {
+                const float* vp = &Vs[min(16 * rt + cl, R - 1) * LDSW + h * DH + (DH / 4) * kq];
+                f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < DH / 4; m += 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(vp + m);
+                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, wb[m + 0], a4, 0, 0, 0);
+                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, wb[m + 1], a4, 0, 0, 0);
+                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, wb[m + 2], a4, 0, 0, 0);
+                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, wb[m + 3], a4, 0, 0, 0);
+                    if (m % 16 == 12) __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 16 * rt + 4 * kq + i;
+                    if (r < R) VW[r * LDSW + col] = a4[i];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            softmax(h);
+            __syncthreads();
+            // acc[t] += P[rows of tile t][action j] VW_h[N + j][col]; k-step m of lane group kq
+            // is action j = (N/4) kq + m
+            if (!(RSA_ABLATE & 4)) {
+                float bv[N / 4];
+#pragma unroll
+                for (int m = 0; m < N / 4; ++m) bv[m] = VW[(N + (N / 4) * kq + m) * LDSW + col];
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) {
+                    const float* ap = &P[(16 * t + cl) * PS + PG * kq];
+#if RSA_P_WIDE
+                    const float4 a4 = *reinterpret_cast<const float4*>(ap);
+                    const float a5 = ap[4];
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[0], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[1], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[2], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, bv[3], acc[t], 0, 0, 0);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a5, bv[4], acc[t], 0, 0, 0);
+#else
+#pragma unroll
+                    for (int m = 0; m < N / 4; ++m)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m], bv[m], acc[t], 0, 0, 0);
+#endif
+                    // keep the scheduler from hoisting every tile's A reads (register blow-up)
+                    if (RSA_GEMM_SCHED_BARRIER && t % 5 == 4) __builtin_amdgcn_sched_barrier(0);
+                }
+                // the state row of each set: rows 16t + 4kq + i (i < 4) belong to one set s
+#pragma unroll
+                for (int t = 0; t < TILES; ++t) {
+                    const int row0 = 16 * t + 4 * kq + z;
+                    const int s_ = row0 / N;
+                    const float4 p0 = *reinterpret_cast<const float4*>(&P0[row0]);
+                    const float vws = VW[s_ * LDSW + col];
+                    acc[t][0] += p0.x * vws;
+                    acc[t][1] += p0.y * vws;
+                    acc[t][2] += p0.z * vws;
+                    acc[t][3] += p0.w * vws;
+                    if (t % 5 == 4) __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            __syncthreads();
+        }
+        // ---- epilogue per group of 4 sets: bias + residual, LayerNorm, mean over the set
+#pragma unroll
+        for (int g = 0; g < GROUPS; ++g) {
+#pragma unroll
+            for (int tt = 0; tt < SETS * N / 16; ++tt) {
+                const int t = g * (SETS * N / 16) + tt;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * t + 4 * kq + i + z;      // set row of the env
+                    const int s_ = row / N, r = row - s_ * N;
+                    const float xr = Xs[member(SWARM_RSA_BASELINES, N, s_, r) * LDSW + col];
+                    PF[(row - g * SETS * N) * LDSW + col] = (acc[t][i] + bias) + xr;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+            const int wave = w & (SETS - 1), half = w >> 2;
+            // row statistics: 4 lanes per row (32 columns each), quad reductions (DPP)
+            if (tid < 4 * SETS * N && !(RSA_ABLATE & 16)) {
+                const int row = tid >> 2, part = tid & 3;
+                const float4* fr = reinterpret_cast<const float4*>(&PF[row * LDSW + 32 * part]);
+                float4 v[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) v[c] = fr[c];
+                float sum = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) sum += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+                sum += __shfl_xor(sum, 1, 4);
+                sum += __shfl_xor(sum, 2, 4);
+                const float mean = sum * (1.0f / HD);
+                float sq = 0.0f;
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const float d0 = v[c].x - mean, d1 = v[c].y - mean, d2 = v[c].z - mean, d3 = v[c].w - mean;
+                    sq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+                }
+                sq += __shfl_xor(sq, 1, 4);
+                sq += __shfl_xor(sq, 2, 4);
+                if (part == 0) {
+                    stats[2 * row] = mean;
+                    stats[2 * row + 1] = 1.0f / sqrtf(sq * (1.0f / HD) + 1e-5f);
+                }
+            }
+            __syncthreads();
+            if (!(RSA_ABLATE & 16)) {
+                const int pc = 64 * half + lane;
+                const float* st = &stats[wave * 2 * N];   // rows wave * N + r of the group
+                float p0 = 0.0f;
+#pragma unroll 4
+                for (int r = 0; r < N; ++r) p0 += (PF[(wave * N + r) * LDSW + pc] - st[2 * r]) * st[2 * r + 1];
+                pooled[((size_t)e * N + g * SETS + wave) * HD + pc] = p0 / (float)N;
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // LayerNorm without affine (eps 1e-5) of 128-wide rows: 32 lanes x float4 per
 // row, 8 rows per 256-thread block; one HBM read and one write per element.
 __global__ void __launch_bounds__(256) embedding_norm_kernel(int64_t rows, const float4* __restrict__ in,
@@ -371,9 +675,11 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
     const int grid = iters < g_cus ? iters : g_cus;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool n20 = N == NMAX;  // the reference swarm: compile-time set size
+    const bool shared_vw = RSA_SHARED_VW && n20 && mode == SWARM_RSA_BASELINES;
 #define RSA_LAUNCH(NH)                                                                                   \
-    (n20 ? rsa_pool_kernel<NH, NMAX><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)       \
-         : rsa_pool_kernel<NH, 0><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
+    (shared_vw ? rsa_baselines_kernel<NH><<<grid, NT, 0, s>>>(B, x, qkv, w_out, b_out, pooled)            \
+     : n20     ? rsa_pool_kernel<NH, NMAX><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)   \
+               : rsa_pool_kernel<NH, 0><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
     if (heads == 1)
         RSA_LAUNCH(1);
     else if (heads == 2)

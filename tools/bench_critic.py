@@ -89,11 +89,20 @@ def main():
     fc_flops = 2.0 * N * N * h * h            # fc_out over the N sets x N rows
     other = 2.0 * R * R * h + 2.0 * N ** 3 * h  # pair logits (all heads) + P.V
     flops = E * (fc_flops + other)
+    # What rsa_baselines_kernel issues instead (fc_out folded into the values, swarm_critic.hip):
+    # logits, V_h W_o,h^T for the 2N rows (48 padded), and one (N*N) x N x h product per head,
+    # as 16x16x4 f32 MFMAs (2048 flops each); the state-row term is VALU
+    tiles = lambda a: (a + 15) // 16  # noqa: E731
+    mfmas = H * tiles(R) ** 2 * (h // H // 4) + tiles(R) * (h // 16) * (h // 4) + H * (N * N // 16) * (h // 16) * (N // 4)
     print(json.dumps({"stage": "rsa_pool_kernel", "ms": sec * 1e3, "algorithmic_flops": flops,
+                      "executed_mfma_flops": E * mfmas * 2048.0,
                       "roofline": {"bound": "mfma", "achieved": flops / sec / 1e12, "peak": MFMA_F32_PEAK,
                                    "unit": "TFLOP/s", "frac": flops / sec / 1e12 / MFMA_F32_PEAK,
+                                   "executed_mfma_tflops": E * mfmas * 2048.0 / sec / 1e12,
                                    # logits, P.V and fc_out all run on v_mfma_f32_16x16x4_f32
                                    "mfma_share_of_flops": 1.0},
+                      "note": "achieved = the reference algorithm's flops / kernel time; the kernel "
+                              "executes executed_mfma_flops (fc_out folded into the values)",
                       "config": cfg}), flush=True)
 
     # ---- what the rollout calls per decision (no_grad), fused vs PyTorch path
