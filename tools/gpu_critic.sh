@@ -13,7 +13,7 @@ timeout -k 10 300 python3 bench.py --critic > gpurun_out/bench_critic.log 2>&1 |
 cat gpurun_out/bench_critic.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_critic -o run --output-format csv -- \
   python3 bench.py --critic --cpu-envs 1 > gpurun_out/prof_critic.log 2>&1 || { tail -20 gpurun_out/prof_critic.log; exit 6; }
-timeout -s KILL 120 rocprofv3 --kernel-include-regex rsa_pool --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+timeout -s KILL 120 rocprofv3 --kernel-include-regex "rsa_(pool|baselines)" --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
   -d gpurun_out/pmc_critic -o run --output-format csv -- python3 bench.py --critic --cpu-envs 1 --reps 3 \
   > gpurun_out/pmc_critic.log 2>&1 || { tail -20 gpurun_out/pmc_critic.log; exit 7; }
 echo CRITIC_DONE
