@@ -90,92 +90,93 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const fl
                                                           const float* __restrict__ dh_n,
                                                           const float* __restrict__ dc_n, float* __restrict__ dxg,
                                                           float* __restrict__ dh0, float* __restrict__ dc0) {
-    __shared__ float dgs[4 * MAXU];
-    __shared__ float part[4 * MAXU];
-    __shared__ float dhr[MAXU];
+    __shared__ __attribute__((aligned(16))) float dgs[4 * MAXU];
+    __shared__ __attribute__((aligned(16))) float part[4 * MAXU];
     const int64_t b = blockIdx.x;
     const int j = threadIdx.x;
     const int G = 4 * U;
-    // thread j < G sums quarter q = j / U of the gate rows for unit u = j % U:
-    // dh_prev'[u] = sum_{r} W_hh[r][u] dgates[r]
+    // thread j < G is gate row j = q U + u in phase 1 (its gate's gradient) and, in phase 2,
+    // sums quarter q of the gate rows for unit u: dh_prev'[u] = sum_r W_hh[r][u] dgates[r]
     const int q = j / (U > 0 ? U : 1), u = j - q * U;
+    const bool act_j = j < G;
     float wt[MAXU];
 #pragma unroll
-    for (int m = 0; m < MAXU; ++m) wt[m] = (j < G && m < U) ? w_hh[(q * U + m) * U + u] : 0.0f;
-    float dc_rec = 0.0f, dc_prev = 0.0f;
-    if (j < U) {
-        dhr[j] = dh_n ? dh_n[b * U + j] : 0.0f;
-        dc_rec = dc_n ? dc_n[b * U + j] : 0.0f;
-    }
-    // a step's saved activations / cells / output gradient, loaded one step ahead of use
+    for (int m = 0; m < MAXU; ++m) wt[m] = (act_j && m < U) ? w_hh[(q * U + m) * U + u] : 0.0f;
+    // the recurrent gradients of unit u, kept (identically) by its four threads
+    float dh_rec = (act_j && dh_n) ? dh_n[b * U + u] : 0.0f;
+    float dc_rec = (act_j && dc_n) ? dc_n[b * U + u] : 0.0f;
+    // a step's saved activations / cells / output gradient of unit u, loaded one step ahead
     struct StepIn {
         float ig, fg, gg, og, ct, cp, kprev, dh;
     };
     auto load = [&](int t) {
         StepIn v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
-        if (j < U) {
+        if (act_j) {
             const int64_t row = b * T + t;
             const float* a = act + row * G;
-            v.ig = a[j];
-            v.fg = a[U + j];
-            v.gg = a[2 * U + j];
-            v.og = a[3 * U + j];
-            v.ct = c_out[row * U + j];
+            v.ig = a[u];
+            v.fg = a[U + u];
+            v.gg = a[2 * U + u];
+            v.og = a[3 * U + u];
+            v.ct = c_out[row * U + u];
             v.kprev = (t > 0 && keep) ? keep[row - 1] : 1.0f;
-            v.cp = t > 0 ? c_out[(row - 1) * U + j] : c0[b * U + j];
-            v.dh = dh_out[row * U + j];
+            v.cp = t > 0 ? c_out[(row - 1) * U + u] : c0[b * U + u];
+            v.dh = dh_out[row * U + u];
         }
         return v;
     };
     StepIn nxt = load(T - 1);
-    __syncthreads();
+    float k_after = 1.0f;   // keep between this step and the next one (applied to the parts)
+    float dc_prev = 0.0f;
     for (int t = T - 1; t >= 0; --t) {
         const int64_t row = b * T + t;
         const StepIn in = nxt;
         if (t > 0) nxt = load(t - 1);
-        if (j < U) {
+        if (act_j) {
+            if (t < T - 1)   // dh_prev' of step t + 1, masked by the keep between t and t + 1
+                dh_rec = ((part[u] + part[U + u]) + (part[2 * U + u] + part[3 * U + u])) * k_after;
             const float cp = t > 0 ? in.cp * in.kprev : in.cp;
-            const float dh = in.dh + dhr[j];
+            const float dh = in.dh + dh_rec;
             const float tc = tanhf(in.ct);
             const float dc = dc_rec + dh * in.og * (1.0f - tc * tc);
-            const float gi = dc * in.gg * in.ig * (1.0f - in.ig);
-            const float gf = dc * cp * in.fg * (1.0f - in.fg);
-            const float gg2 = dc * in.ig * (1.0f - in.gg * in.gg);
-            const float go = dh * tc * in.og * (1.0f - in.og);
-            dgs[j] = gi;
-            dgs[U + j] = gf;
-            dgs[2 * U + j] = gg2;
-            dgs[3 * U + j] = go;
-            float* d = dxg + row * G;
-            d[j] = gi;
-            d[U + j] = gf;
-            d[2 * U + j] = gg2;
-            d[3 * U + j] = go;
+            float gq;
+            if (q == 0) gq = dc * in.gg * in.ig * (1.0f - in.ig);
+            else if (q == 1) gq = dc * cp * in.fg * (1.0f - in.fg);
+            else if (q == 2) gq = dc * in.ig * (1.0f - in.gg * in.gg);
+            else gq = dh * tc * in.og * (1.0f - in.og);
+            dgs[j] = gq;
+            dxg[row * G + j] = gq;
             dc_prev = dc * in.fg;
+            dc_rec = dc_prev * in.kprev;
+            k_after = in.kprev;
         }
         __syncthreads();
-        if (j < G) {
+        if (act_j) {
             float s0 = 0.0f, s1 = 0.0f;
+            if ((U & 3) == 0) {   // quarter rows start 16 B aligned: float4 reads (wt is 0 past U)
+                const float4* dg4 = reinterpret_cast<const float4*>(&dgs[q * U]);
 #pragma unroll
-            for (int m = 0; m < MAXU; m += 2)
-                if (m < U) {
-                    s0 += wt[m] * dgs[q * U + m];
-                    if (m + 1 < U) s1 += wt[m + 1] * dgs[q * U + m + 1];
-                }
+                for (int m = 0; m < MAXU; m += 4)
+                    if (m < U) {
+                        const float4 d = dg4[m / 4];
+                        s0 += wt[m] * d.x + wt[m + 2] * d.z;
+                        s1 += wt[m + 1] * d.y + wt[m + 3] * d.w;
+                    }
+            } else {
+#pragma unroll
+                for (int m = 0; m < MAXU; m += 2)
+                    if (m < U) {
+                        s0 += wt[m] * dgs[q * U + m];
+                        if (m + 1 < U) s1 += wt[m + 1] * dgs[q * U + m + 1];
+                    }
+            }
             part[j] = s0 + s1;
         }
         __syncthreads();
-        if (j < U) {
-            const float dhp = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
-            if (t > 0) {
-                dhr[j] = dhp * in.kprev;
-                dc_rec = dc_prev * in.kprev;
-            } else {
-                if (dh0) dh0[b * U + j] = dhp;
-                if (dc0) dc0[b * U + j] = dc_prev;
-            }
-        }
-        __syncthreads();
+    }
+    if (j < U) {
+        if (dh0) dh0[b * U + j] = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
+        if (dc0) dc0[b * U + j] = dc_prev;
     }
 }
 
