@@ -1,0 +1,108 @@
+"""PPO optimizer steps replayed from a HIP graph.
+
+A trainer's optimizer step (forward of every network over one minibatch, the
+loss, backward and Adam) is a few hundred small kernels whose launch cost on
+the host exceeds their GPU time at the ML-Agents minibatch sizes. `GraphedStep`
+runs the first steps of a trainer eagerly (they warm up the allocator, the
+library handles and the optimizer state, and they ARE training steps), then
+captures the step once with torch.cuda.graph over static copies of the
+minibatch tensors and replays it for every later minibatch of the same
+structure. A minibatch of another structure (the last, ragged one of an epoch)
+runs eagerly. The step function must not synchronise with the host; its
+Python-side constants (clip epsilon, entropy beta, learning rate) are part of
+the capture, so `GraphedStep.key` holds them and a new key recaptures.
+
+The optimizers are switched to `capturable=True` (their step counters live on
+the device); the same kernels then run eagerly and in the graph, so a graphed
+update equals the eager one (tests/test_gpu_graph_step.py).
+"""
+
+from __future__ import annotations
+
+import os
+import traceback
+import warnings
+
+import torch
+
+# SWARM_GRAPHS=0 forces eager steps
+ENABLED = os.environ.get("SWARM_GRAPHS", "1") != "0"
+
+
+def make_capturable(optimizers, device: torch.device):
+    """capturable=True for every param group; existing step counters move to the device."""
+    for opt in optimizers:
+        for pg in opt.param_groups:
+            pg["capturable"] = True
+        for st in opt.state.values():
+            s = st.get("step")
+            if isinstance(s, torch.Tensor) and s.device != device:
+                st["step"] = s.to(device=device, dtype=torch.float32)
+
+
+class GraphedStep:
+    """fn(batch: dict[str, Tensor]) -> Tensor (detached per-step outputs)."""
+
+    def __init__(self, fn, warmup: int = 2):
+        self.fn = fn
+        self.warmup = warmup
+        self.eager_done = 0
+        self.graph = None
+        self.sig = None
+        self.key = None
+        self.static = None
+        self.out = None
+        self.replays = 0
+        self.failed = False
+
+    @staticmethod
+    def signature(batch: dict):
+        return tuple((k, tuple(v.shape), v.dtype, v.device) for k, v in sorted(batch.items()))
+
+    def reset(self, key=None):
+        """Drop the captured graph (new constants); later steps recapture without warmup."""
+        self.graph = None
+        self.static = None
+        self.out = None
+        self.key = key
+
+    def __call__(self, batch: dict, key=None) -> torch.Tensor:
+        if key != self.key:
+            self.reset(key)
+        sig = self.signature(batch)
+        if self.graph is not None and sig == self.sig:
+            for k, v in batch.items():
+                self.static[k].copy_(v)
+            self.graph.replay()
+            self.replays += 1
+            return self.out
+        if self.eager_done < self.warmup or (self.graph is not None and sig != self.sig):
+            # warm-up (side stream, as torch.cuda.graph requires) or a minibatch of another shape
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                out = self.fn(batch)
+            torch.cuda.current_stream().wait_stream(s)
+            self.eager_done += 1
+            return out
+        if self.failed:
+            return self.fn(batch)
+        # capture this structure, then replay it for this minibatch. Capture records and
+        # does not execute, so a step that cannot be captured (an op that synchronises)
+        # leaves the parameters untouched: it then runs eagerly, as do all later steps.
+        self.static = {k: v.clone() for k, v in batch.items()}
+        self.sig = sig
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(self.graph):
+                self.out = self.fn(self.static)
+        except RuntimeError as e:   # torch.AcceleratorError derives from RuntimeError
+            where = "".join(traceback.format_exception(e)[-8:-1])
+            warnings.warn(f"optimizer step not capturable, running eagerly: {e}\n{where}")
+            self.failed = True
+            self.reset(self.key)
+            torch.cuda.synchronize()
+            return self.fn(batch)
+        self.graph.replay()
+        self.replays += 1
+        return self.out

@@ -17,6 +17,7 @@ from pathlib import Path
 import torch
 
 from .distributed import TrainerComm
+from . import _graph
 from .metrics import make_writer
 
 
@@ -155,6 +156,26 @@ class TrainerBase:
                 self.buffer.sequence_batch_count(self.cfg.sequence_length, mb)))
         return it
 
+    # ------------------------------------------------------------ graphed steps
+    def _graphs_ok(self) -> bool:
+        """Replay optimizer steps from a HIP graph (agents/_graph.py): single process on
+        a ROCm device, no per-step test hooks."""
+        return (_graph.ENABLED and self.device.type == "cuda" and not self.comm.active
+                and self.grad_hook is None and self.step_hook is None)
+
+    def _step_runner(self, step_fn, optimizers):
+        """A callable batch -> detached loss terms: GraphedStep over step_fn when graphs
+        are usable, else step_fn itself. The runner (and its graph) persists across updates;
+        it recaptures when the key (schedule values) changes."""
+        if not self._graphs_ok():
+            return lambda batch, key=None: step_fn(batch)
+        if getattr(self, "_graphed", None) is None:
+            _graph.make_capturable(optimizers, self.device)
+            # the warm-up steps only matter for the trainer's first capture
+            self._graphed = _graph.GraphedStep(step_fn, warmup=0 if getattr(self, "_graph_warm", False) else 2)
+            self._graph_warm = True
+        return self._graphed
+
     def optimizer_step(self, loss: torch.Tensor, step_index: int):
         self.comm.zero_grad(self.optimizer)
         loss.backward()
@@ -268,6 +289,9 @@ class TrainerBase:
         print(f"[{self.algo}] Saved -> {path}")
 
     def _rebind_grads(self):
+        """After loading parameters / optimizer state: a captured step graph refers to the
+        replaced optimizer tensors, so it is dropped (the next update recaptures)."""
+        self._graphed = None
         if self.comm.flat_grad is not None:   # optimizer state loaded; keep grads bound to the flat buffer
             self.comm.bind_flat_grads(self.params)
 

@@ -211,6 +211,13 @@ class FixedOptionCriticTrainer(TrainerBase):
                 - current_beta * oe - c.termination_entropy_coef * te)
 
     # ------------------------------------------------------------ update
+    def _ppo_step(self, batch: dict) -> torch.Tensor:
+        """One optimizer step -> the LOSS_KEYS terms (detached); eps / beta / lr are read
+        here, so a graph capture holds this update's values."""
+        losses = self.compute_losses(batch, self.current_eps)
+        self.optimizer_step(self.total_loss(losses, self.current_beta), getattr(self, "_step_index", 0))
+        return torch.stack([x.detach().reshape(()) for x in losses])
+
     def update(self) -> dict:
         """option_critic_trainer.py:668-757."""
         cfg = self.cfg
@@ -220,11 +227,12 @@ class FixedOptionCriticTrainer(TrainerBase):
         self.comm.normalize_(self.buffer.advantages[:T])
         totals = torch.zeros(len(LOSS_KEYS), dtype=torch.float64, device=self.device)
         n_updates = 0
+        step = self._step_runner(self._ppo_step, [self.optimizer])
+        key = (eps, beta, self.current_lr)
         for _epoch in range(cfg.num_epochs):
             for batch in self._sequence_batches():
-                losses = self.compute_losses(batch, eps)
-                self.optimizer_step(self.total_loss(losses, beta), n_updates)
-                totals += torch.stack([x.detach().reshape(()) for x in losses]).double()
+                self._step_index = n_updates
+                totals += step(batch, key).double()
                 n_updates += 1
         self.update_count += 1
         counts = torch.bincount(self.buffer.options[:T].reshape(-1), minlength=cfg.num_options).double()

@@ -399,10 +399,21 @@ class POCACritic(nn.Module):
 
     # ------------------------------------------------------------ helpers
     def _norm_agent_count(self, n: int, B: int, device) -> torch.Tensor:
-        """n in [-1, 1] against the largest n seen (poca_networks.py:579-584)."""
-        if n > self._current_max_agents.item():
-            self._current_max_agents.data.fill_(float(n))
-        return torch.full((B, 1), n * 2.0 / self._current_max_agents.item() - 1.0, device=device)
+        """n in [-1, 1] against the largest n seen (poca_networks.py:579-584). The running
+        max is mirrored on the host, keyed by the parameter's version counter (any in-place
+        write, incl. load_state_dict, re-reads it), so a pass does not synchronise with the
+        device (and can be captured in a graph)."""
+        t = self._current_max_agents
+        cached = getattr(self, "_max_agents_host", None)
+        if cached is None or cached[0] != t._version:
+            cached = (t._version, float(t.item()))
+        m = cached[1]
+        if n > m:
+            t.data.fill_(float(n))
+            m = float(n)
+            cached = (t._version, m)
+        self._max_agents_host = cached
+        return torch.full((B, 1), n * 2.0 / m - 1.0, device=device)
 
     def initial_state(self, batch_size: int, device):
         if self.lstm is None:
@@ -502,11 +513,14 @@ class POCACritic(nn.Module):
         B, N, _ = all_states.shape
         rows = torch.arange(B, device=all_states.device)
         focal = focal_agent_ids.long()
-        keep = torch.ones(B, N, dtype=torch.bool, device=all_states.device)
-        keep[rows, focal] = False
-        return self.baseline(all_states[rows, focal], all_states[keep].view(B, N - 1, self.state_dim),
-                             all_actions[keep].view(B, N - 1, self.act_dim), memory, sequence_length,
-                             return_memory)
+        # the other agents in increasing order, as the reference's boolean-mask select, by
+        # index (no device -> host sync): other k = k + (k >= focal)
+        k = torch.arange(N - 1, device=all_states.device).unsqueeze(0)
+        others = (k + (k >= focal.unsqueeze(1)).long()).unsqueeze(-1)
+        return self.baseline(all_states[rows, focal],
+                             all_states.gather(1, others.expand(B, N - 1, all_states.shape[-1])),
+                             all_actions.gather(1, others.expand(B, N - 1, all_actions.shape[-1])), memory,
+                             sequence_length, return_memory)
 
     def decision_passes(self, all_states, all_actions, *, value: bool = True, joint: bool = False,
                         baselines: bool = True, value_memory=None, joint_memory=None, baseline_memory=None):
@@ -560,8 +574,11 @@ class POCACritic(nn.Module):
         if self._fused(all_states, N):
             pooled = _fused_rsa(self.self_attn, torch.cat([obs_emb, act_emb], dim=1), _native.RSA_BASELINES, N)
         else:
-            others = ~torch.eye(N, dtype=torch.bool, device=all_states.device)
-            peers = act_emb.unsqueeze(1).expand(B, N, N, self.h_size)[:, others].view(B, N, N - 1, self.h_size)
+            # peers of set i: entities j != i in increasing j (the reference's ~eye mask), by
+            # index: j = k + (k >= i), so no boolean-mask select (device -> host sync)
+            i = torch.arange(N, device=all_states.device).unsqueeze(1)
+            k = torch.arange(N - 1, device=all_states.device).unsqueeze(0)
+            peers = act_emb[:, k + (k >= i).long()]                      # (B, N, N - 1, h)
             sets = torch.cat([obs_emb.unsqueeze(2), peers], dim=2).reshape(B * N, N, self.h_size)
             pooled = self.self_attn(sets)
         result = self._value_tail(pooled, N, memory, sequence_length, return_memory)

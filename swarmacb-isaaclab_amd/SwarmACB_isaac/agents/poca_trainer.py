@@ -122,8 +122,10 @@ class POCATrainer(TrainerBase):
         obs, critic_states = batch["obs"], batch["critic_states"]
         new_logp, entropy = self.actor.evaluate(obs, batch["actions"])
         B = obs.shape[0]
-        d_pol, d_row = self._denominators([torch.tensor(float(new_logp.numel()), device=obs.device),
-                                           torch.tensor(float(B), device=obs.device)])
+        d_pol = d_row = None   # single process: the reference's means (no host -> device count tensors)
+        if self.comm.active:
+            d_pol, d_row = self._denominators([torch.tensor(float(new_logp.numel()), device=obs.device),
+                                               torch.tensor(float(B), device=obs.device)])
         policy_loss = trust_region_policy_loss(batch["advantages"].unsqueeze(-1), new_logp, batch["old_log_probs"],
                                                current_eps, denom=d_pol)
         mean_entropy = entropy.mean() if d_row is None else entropy.sum() / d_row
@@ -197,6 +199,14 @@ class POCATrainer(TrainerBase):
             it = itertools.islice(it, self.comm.min_int(self.buffer.flat_batch_count(mb)))
         return it
 
+    def _ppo_step(self, batch: dict) -> torch.Tensor:
+        """One optimizer step (PT:806-834) -> the four loss terms (detached); the clip
+        epsilon, beta and lr are read here, so a graph capture holds this update's values."""
+        pl, vl, bl, ent = self.compute_losses(batch, self.current_eps)
+        loss = pl + 0.5 * (vl + 0.5 * bl) - self.current_beta * ent
+        self.optimizer_step(loss, getattr(self, "_step_index", 0))
+        return torch.stack([pl.detach(), vl.detach(), bl.detach(), ent.detach()])
+
     def update(self) -> dict:
         """poca_trainer.py:781-852: num_epochs x minibatches of the buffer."""
         cfg = self.cfg
@@ -206,12 +216,12 @@ class POCATrainer(TrainerBase):
         self.comm.normalize_(self.buffer.advantages[:T])
         totals = torch.zeros(4, dtype=torch.float64, device=self.device)
         n_updates = 0
+        step = self._step_runner(self._ppo_step, [self.optimizer])
+        key = (eps, beta, self.current_lr)
         for epoch in range(cfg.num_epochs):
             for batch in self._batches(epoch):
-                pl, vl, bl, ent = self.compute_losses(batch, eps)
-                loss = pl + 0.5 * (vl + 0.5 * bl) - beta * ent
-                self.optimizer_step(loss, n_updates)
-                totals += torch.stack([pl.detach(), vl.detach(), bl.detach(), ent.detach()]).double()
+                self._step_index = n_updates
+                totals += step(batch, key).double()
                 n_updates += 1
         self.update_count += 1
         if self.comm.active:

@@ -67,7 +67,7 @@ def main():
     ap.add_argument("--envs", type=int, default=0, help="envs per GPU (0 = the config's)")
     ap.add_argument("--decisions", type=int, default=0, help="rollout decisions (0 = sequence_length)")
     ap.add_argument("--minibatches", type=int, default=8, help="minibatches per epoch in the timed update")
-    ap.add_argument("--warmup-minibatches", type=int, default=2)
+    ap.add_argument("--warmup-minibatches", type=int, default=4)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--matmul-precision", default=None, help="override the config's matmul_precision (OC2)")
     args, _ = ap.parse_known_args()
@@ -121,27 +121,27 @@ def run(name, args):
 
     orig = tr._sequence_batches
     cap = {"n": args.warmup_minibatches}
-    tr._sequence_batches = lambda: itertools.islice(orig(), cap["n"])
+    steps = {"n": 0}
+
+    def capped():
+        for b in itertools.islice(orig(), cap["n"]):
+            steps["n"] += 1
+            yield b
+    tr._sequence_batches = capped
     epochs = cfg.num_epochs
     cfg.num_epochs = 1
-    tr.update()                                   # warm-up minibatches (untimed)
+    # warm-up minibatches (untimed): allocator, library heuristics and, with graphed steps,
+    # the eager warm-up steps and the capture (the timed update replays the same graph)
+    tr.update()
     torch.cuda.synchronize()
     cfg.num_epochs = epochs
     cap["n"] = args.minibatches
-    steps = {"n": 0}
-    if hasattr(tr, "optimizer_step"):
-        real_step = tr.optimizer_step
-
-        def counting(loss, i):
-            steps["n"] += 1
-            return real_step(loss, i)
-        tr.optimizer_step = counting
+    steps["n"] = 0
     t0 = time.perf_counter()
     metrics = tr.update()
     torch.cuda.synchronize()
     t_upd = time.perf_counter() - t0
-    n_steps = steps["n"] or int(metrics.get("critic_updates", 0)) or cfg.num_epochs * min(args.minibatches,
-                                                                                          n_batches_here)
+    n_steps = steps["n"]
     ms_dec = t_roll / R * 1e3
     ms_step = t_upd / n_steps * 1e3
     iter_s = T_ep * ms_dec / 1e3 + steps_ep * ms_step / 1e3
@@ -152,6 +152,7 @@ def run(name, args):
         "agent_steps_per_s_rollout": E * N * dp / (ms_dec / 1e3),
         "minibatch_rows": cfg.mini_batch_size, "sequence_length": L, "sequences_per_minibatch": per_batch,
         "timed_optimizer_steps": n_steps, "ms_per_optimizer_step": ms_step,
+        "graphed_steps": bool(getattr(tr, "_graphed", None) is not None and tr._graphed.replays > 0),
         "reference_update": {"episode_decisions": T_ep, "optimizer_steps": steps_ep,
                              "projected_update_s": steps_ep * ms_step / 1e3,
                              "projected_rollout_s": T_ep * ms_dec / 1e3, "projected_iteration_s": iter_s,
