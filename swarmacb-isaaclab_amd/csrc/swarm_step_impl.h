@@ -61,6 +61,11 @@
 #define SWARM_SOLVE_SHORTCUTS 1
 #endif
 
+// 1: single-wave workgroups exchange through LDS without hardware waits (sync_wg)
+#ifndef SWARM_WAVE_SYNC
+#define SWARM_WAVE_SYNC 1
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -214,9 +219,19 @@ struct Shared {
     float4 red[4][64 * ly_waves(LY)];
 };
 
+// Workgroup-wide exchange point of the LDS tile / partial slots. With one wave
+// per workgroup (layouts 1 and 103) the wave's LDS instructions execute in
+// program order, so a later read sees an earlier write without waiting for it:
+// only the compiler must keep the order (wave-scope fence + wave barrier, no
+// s_waitcnt / s_barrier). Multi-wave layouts need the real barrier.
 template <int LY>
 __device__ __forceinline__ void sync_wg() {
-    __syncthreads();
+    if constexpr (ly_waves(LY) == 1 && SWARM_WAVE_SYNC) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
 }
 
 __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
@@ -670,9 +685,13 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         for (int k = 0; k < 8; ++k) {
             const float proj = rdx[k] * dx + rdy[k] * dy;
             const float csq = dsq - proj * proj;
+            const bool pre = (proj > 0.0f) & (csq <= g.r2);
+            // a disc spans at most two of the 45-degree rays: the wave skips the rest
+            // (a ray no active lane can hit leaves every reading unchanged)
+            if (SWARM_WALL_FILTER && !__any(pre)) continue;
             const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
             const float hd = fmaxf(proj - hc, 0.0f);
-            const bool hit = (proj > 0.0f) & (csq <= g.r2) & (hd <= g.prox_range);
+            const bool hit = pre & (hd <= g.prox_range);
             const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
