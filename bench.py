@@ -149,18 +149,23 @@ def load_pmc(envs: int, sub: int) -> dict:
 
 
 def prewarm(seconds: float, E: int, dp: int, dev) -> float:
-    """Untimed launches of the same step on a scratch engine for `seconds` (clock ramp-up)."""
+    """Untimed launches of the same workload (same step, same action distribution) on a
+    scratch engine for `seconds`, run right before the warm-up decisions so the clocks
+    are up when the timed region starts."""
     if seconds <= 0:
         return 0.0
     from SwarmACB_isaac.engine import SwarmEngine
 
     eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, 0, 12345, dev)
     out = eng.reset()
-    a = torch.zeros(E, N_AGENTS, 2, device=dev)
+    g = torch.Generator(device=dev).manual_seed(12345)
+    acts = (torch.randn(8, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
     t0 = time.perf_counter()
+    i = 0
     while time.perf_counter() - t0 < seconds:
         for _ in range(20):
-            eng.step(a, dp, out=out)
+            eng.step(acts[i % 8], dp, out=out)
+            i += 1
         torch.cuda.synchronize(dev)
     eng.close()
     return time.perf_counter() - t0
@@ -210,7 +215,6 @@ def main():
     from SwarmACB_isaac.shard import EnvShard, max_over_ranks
 
     E, dp = args.envs, args.decision_period
-    prewarm_s = prewarm(args.prewarm, E, dp, dev)
     shard = EnvShard.weak(E, rank, world)     # weak scaling: E envs per GPU, keyed by global env id
     eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, shard.env_offset, args.seed, dev,
                       layout=args.layout or None)
@@ -224,6 +228,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
     acts = (torch.randn(n_warm + n_dec, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
 
+    prewarm_s = prewarm(args.prewarm, E, dp, dev)
     for d in range(n_warm):
         eng.step(acts[d], dp, out=out)
     torch.cuda.synchronize(dev)

@@ -75,6 +75,19 @@ def stable_trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilo
     return (loss * active).sum() / (denom if denom is not None else active.sum().clamp_min(1.0))
 
 
+_OFFDIAG = {}
+
+
+def _offdiag_index(O: int, device) -> torch.Tensor:
+    """Row-major flat indices of the off-diagonal entries of an O x O matrix (cached per
+    device, built once outside any graph capture)."""
+    key = (O, str(device))
+    if key not in _OFFDIAG:
+        idx = [r * O + c for r in range(O) for c in range(O) if r != c]
+        _OFFDIAG[key] = torch.tensor(idx, dtype=torch.long, device=device)
+    return _OFFDIAG[key]
+
+
 class LearnedOptionCriticTrainer(TrainerBase):
     """Train learned continuous options with collective counterfactual credit (LOT:170-2345)."""
 
@@ -271,8 +284,11 @@ class LearnedOptionCriticTrainer(TrainerBase):
         n_rows = d_rows if d_rows is not None else active.sum().clamp_min(1.0)
         normalized = F.normalize(attentions, p=2, dim=-1, eps=1e-8)
         sim = torch.matmul(normalized, normalized.transpose(-1, -2))
-        off = ~torch.eye(O, dtype=torch.bool, device=attentions.device)
-        diversity = (sim[..., off].sum(-1) * active).sum() / (n_rows * (O * (O - 1)))
+        # the off-diagonal pairs in row-major order, as the reference's boolean mask selects
+        # them, by index (a mask select synchronises with the host)
+        off = torch.arange(O * O, device=attentions.device)
+        off = off[(off // O) != (off % O)] if not attentions.is_cuda else _offdiag_index(O, attentions.device)
+        diversity = (sim.flatten(-2).index_select(-1, off).sum(-1) * active).sum() / (n_rows * (O * (O - 1)))
         pairs = (loss_mask[:, :-1] & loss_mask[:, 1:] & (dones[:, :-1] < 0.5)).to(attentions.dtype)
         n_pairs = d_pairs if d_pairs is not None else pairs.sum().clamp_min(1.0)
         delta = (attentions[:, 1:] - attentions[:, :-1]).abs().mean(dim=(-1, -2))
@@ -316,8 +332,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         sel_w = loss_mask.unsqueeze(-1).to(dtype=option_dist.probs.dtype)
         marginal = ((option_dist.probs * sel_w).sum(dim=(0, 1)) / sel_w.sum().clamp_min(1.0)).clamp_min(1e-8)
         option_marginal_entropy = -(marginal * marginal.log()).sum()
-        option_balance_loss = (marginal * (marginal.log() + torch.log(torch.tensor(
-            float(O), device=marginal.device, dtype=marginal.dtype)))).sum()
+        option_balance_loss = (marginal * (marginal.log() + self._log_const(float(O), marginal))).sum()
         effective_options = option_marginal_entropy.exp()
         selector_loss = option_values.sum() * 0.0
         option_approx_kl = option_values.sum() * 0.0
@@ -428,6 +443,15 @@ class LearnedOptionCriticTrainer(TrainerBase):
             "behavior_option_logp_error": behavior_option_logp_error,
         }
 
+    def _log_const(self, value: float, like: torch.Tensor) -> torch.Tensor:
+        """torch.log(torch.tensor(value)) on like's device / dtype, made once (a host ->
+        device copy per minibatch would also keep the step from being graphed)."""
+        cache = self.__dict__.setdefault("_log_consts", {})
+        key = (value, like.device, like.dtype)
+        if key not in cache:
+            cache[key] = torch.log(torch.tensor(value, device=like.device, dtype=like.dtype))
+        return cache[key]
+
     def compute_losses(self, batch: dict, current_eps: float, reference_actor=None) -> dict:
         return self._compute_sequence_losses(batch, current_eps, reference_actor or self.reference_actor)
 
@@ -465,6 +489,116 @@ class LearnedOptionCriticTrainer(TrainerBase):
             self.step_hook((kind, index), params)
         return norm
 
+    # ------------------------------------------------------------ graphed update
+    def _init_adam_state(self, optimizer):
+        """Create the Adam state the first step would create (zeros, device step counter), so
+        a captured step can save and restore it."""
+        for group in optimizer.param_groups:
+            for p in group["params"]:
+                st = optimizer.state[p]
+                if "step" not in st:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+
+    def _actor_step_tensors(self):
+        st = self.actor_optimizer.state
+        out = []
+        for p in self.actor_parameters:
+            out += [p, st[p]["step"], st[p]["exp_avg"], st[p]["exp_avg_sq"]]
+        return out
+
+    def _clip_step_device(self, loss, comm, optimizer, params, max_norm: float):
+        """_clip_step without host synchronisation (finiteness is checked after the update)."""
+        comm.zero_grad(optimizer)
+        loss.backward()
+        comm.all_reduce_grads()
+        norm = torch.nn.utils.clip_grad_norm_(params, max_norm, error_if_nonfinite=False)
+        optimizer.step()
+        return norm
+
+    def _oc2_step(self, batch: dict) -> torch.Tensor:
+        """One minibatch of update() (LOT:1421-1660) with every decision on the device: the
+        KL early stop is a predicate under which the actor's Adam step is kept or undone
+        (parameters and Adam state restored), finiteness is flagged for a check after the
+        update. Accumulates into self._g (static tensors, so the step can be graphed)."""
+        G, cfg = self._g, self.cfg
+        G["samples"] += batch["loss_mask"].sum()
+        losses = self.compute_losses(batch, self.current_eps, self.reference_actor)
+        terms, actor_loss, critic_loss = self.objectives(losses)
+        kl = torch.stack([losses["action_approx_kl"].detach(), losses["option_approx_kl"].detach()]).double()
+        policy_kl = torch.maximum(kl[0], kl[1])
+        G["init_kl"].copy_(torch.where(G["nb"] == 0, policy_kl, G["init_kl"]))
+        torch.maximum(G["max_kl"], torch.stack([policy_kl, kl[0], kl[1]]), out=G["max_kl"])
+        over = (policy_kl > 1.5 * cfg.target_kl) if cfg.target_kl > 0.0 else torch.zeros_like(G["stopped"])
+        apply = ~G["stopped"] & ~over
+        G["stopped"] |= over
+        G["bad"][0] |= ~torch.isfinite(actor_loss.detach())
+        G["bad"][1] |= ~torch.isfinite(critic_loss.detach())
+        saved = [t.detach().clone() for t in self._actor_step_tensors()]
+        norm_a = self._clip_step_device(actor_loss, self.actor_comm, self.actor_optimizer, self.actor_parameters,
+                                        cfg.actor_max_grad_norm)
+        with torch.no_grad():
+            for t, b in zip(self._actor_step_tensors(), saved):
+                t.copy_(torch.where(apply, t, b))
+        G["grad_norms"][0] += torch.where(apply, norm_a.double(), torch.zeros_like(G["grad_norms"][0]))
+        G["bad"][2] |= apply & ~torch.isfinite(norm_a)
+        G["actor_updates"] += apply.double()
+        norm_c = self._clip_step_device(critic_loss, self.critic_comm, self.critic_optimizer,
+                                        self.critic_parameters, cfg.max_grad_norm)
+        G["grad_norms"][1] += norm_c.double()
+        G["bad"][3] |= ~torch.isfinite(norm_c)
+        G["totals"] += torch.stack([losses[n].detach().reshape(()).double() for n in METRIC_NAMES]
+                                   + [actor_loss.detach().double(), critic_loss.detach().double()]
+                                   + [terms[n].detach().reshape(()).double() for n in OBJECTIVE_NAMES[2:]])
+        G["nb"] += 1.0
+        return G["nb"]
+
+    def _update_graphed(self) -> dict:
+        """update() with its minibatch steps replayed from a HIP graph (agents/_graph.py):
+        one host read after the last minibatch instead of one per minibatch."""
+        cfg, dev = self.cfg, self.device
+        if getattr(self, "_g", None) is None:
+            f64 = dict(dtype=torch.float64, device=dev)
+            self._g = {"totals": torch.zeros(len(METRIC_NAMES) + len(OBJECTIVE_NAMES), **f64),
+                       "grad_norms": torch.zeros(2, **f64), "samples": torch.zeros((), **f64),
+                       "nb": torch.zeros((), **f64), "actor_updates": torch.zeros((), **f64),
+                       "init_kl": torch.zeros((), **f64), "max_kl": torch.zeros(3, **f64),
+                       "stopped": torch.zeros((), dtype=torch.bool, device=dev),
+                       "bad": torch.zeros(4, dtype=torch.bool, device=dev)}
+        for t in self._g.values():
+            t.zero_()
+        self._init_adam_state(self.actor_optimizer)
+        self._init_adam_state(self.critic_optimizer)
+        step = self._step_runner(self._oc2_step, [self.actor_optimizer, self.critic_optimizer])
+        key = (self.current_eps, self.current_beta, self.current_lr, self.current_actor_lr,
+               self.current_termination_prior_coef, self.current_option_balance_coef)
+        for _epoch in range(cfg.num_epochs):
+            for batch in self._sequence_batches():
+                step(batch, key)
+        G = self._g
+        host = torch.cat([G["nb"].reshape(1), G["actor_updates"].reshape(1), G["init_kl"].reshape(1), G["max_kl"],
+                          G["stopped"].double().reshape(1), G["bad"].double()]).tolist()
+        num_batches, actor_updates, initial_policy_kl = int(host[0]), int(host[1]), host[2]
+        max_policy_kl, max_action_kl, max_option_kl = host[3:6]
+        actor_early_stopped = bool(host[6])
+        bad = host[7:11]
+        if num_batches and initial_policy_kl > 1e-6:
+            raise RuntimeError(f"OC2 update-start policy does not match its frozen reference "
+                               f"(KL={initial_policy_kl:.6g}).")
+        for flag, which in ((bad[0], "actor loss"), (bad[1], "critic loss"), (bad[2], "actor gradient"),
+                            (bad[3], "critic gradient")):
+            if flag:
+                raise FloatingPointError(f"LearnedOC produced a non-finite {which} during the update")
+        if actor_early_stopped and self.comm.rank == 0:
+            print(f"[LearnedOC] Actor PPO early stop: policy KL exceeded {1.5 * cfg.target_kl:.4f}; "
+                  f"centralized critics continue")
+        if actor_updates == 0:
+            raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
+                               "should guarantee at least one safe policy minibatch.")
+        return G["totals"].clone(), G["grad_norms"].clone(), G["samples"].clone(), num_batches, actor_updates, \
+            num_batches, max_policy_kl, max_action_kl, max_option_kl, initial_policy_kl, actor_early_stopped
+
     # ------------------------------------------------------------ update
     def update(self) -> dict:
         """learned_option_critic_trainer.py:1421-1765."""
@@ -481,7 +615,10 @@ class LearnedOptionCriticTrainer(TrainerBase):
         actor_early_stopped = False
         self.reference_actor.load_state_dict(self.actor.state_dict())
         self.reference_actor.eval()
-        for _epoch in range(cfg.num_epochs):
+        if self._graphs_ok():
+            (totals, grad_norms, samples, num_batches, actor_updates, critic_updates, max_policy_kl, max_action_kl,
+             max_option_kl, initial_policy_kl, actor_early_stopped) = self._update_graphed()
+        for _epoch in range(0 if self._graphs_ok() else cfg.num_epochs):
             for batch in self._sequence_batches():
                 samples += batch["loss_mask"].sum()
                 losses = self.compute_losses(batch, self.current_eps, self.reference_actor)
@@ -797,6 +934,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         self.option_critic.load_state_dict(ck["option_critic"])
         self.actor_optimizer.load_state_dict(ck["actor_optimizer"])
         self.critic_optimizer.load_state_dict(ck["critic_optimizer"])
+        self._graphed = None        # a captured step refers to the replaced optimizer tensors
         if self.actor_comm.flat_grad is not None:
             self.actor_comm.bind_flat_grads(self.actor_parameters)
             self.critic_comm.bind_flat_grads(self.critic_parameters)

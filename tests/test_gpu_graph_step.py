@@ -85,3 +85,65 @@ def test_graphed_update_equals_eager(kind, gpu_device, tmp_path, monkeypatch):
             assert graphed_metrics[k] == pytest.approx(v, rel=2e-4, abs=1e-6), k
     print(f"[graph] {kind}: {tr._graphed.replays} replayed steps, max param diff {worst:.3g} of scale")
     env.close()
+
+
+@pytest.mark.parametrize("target_kl", [0.02, 1e-7])
+def test_graphed_oc2_update_equals_eager(target_kl, gpu_device, tmp_path, monkeypatch):
+    """OC2: the graphed update takes the KL early stop as a device predicate (the actor's
+    Adam step undone where it stops); with a normal and a tiny KL budget it must match
+    the eager update's parameters and decisions."""
+    from SwarmACB_isaac.agents import _graph
+    from SwarmACB_isaac.agents.config import LearnedOptionCriticConfig, make_env_cfg
+    from SwarmACB_isaac.agents.learned_option_critic_trainer import LearnedOptionCriticTrainer
+    from SwarmACB_isaac.agents.metrics import NullWriter
+    from SwarmACB_isaac.registry import make
+
+    torch.manual_seed(0)
+    task, variant = "SwarmACB-XOR-v0", "cyclamen"
+    cfg = LearnedOptionCriticConfig(horizon=12, mini_batch_size=256, num_epochs=2, sequence_length=8,
+                                    target_kl=target_kl, log_dir=str(tmp_path))
+    env = make(task, make_env_cfg(task, variant, {"num_envs": 32}, cfg.trainer_type, seed=0), device=gpu_device)
+    tr = LearnedOptionCriticTrainer(env, cfg, writer=NullWriter())
+    obs, _ = env.reset()
+    tr.collect_rollout(obs, cfg.horizon)
+    opts = [tr.actor_optimizer, tr.critic_optimizer]
+    _graph.make_capturable(opts, tr.device)
+    tr._init_adam_state(tr.actor_optimizer)
+    tr._init_adam_state(tr.critic_optimizer)
+    T = tr.buffer.ptr
+    adv0 = tr.buffer.action_advantages[:T].clone()
+    params0 = [p.detach().clone() for p in tr.params]
+    states0 = [copy.deepcopy(o.state_dict()) for o in opts]
+    scale0, rng0 = tr.actor_lr_scale, torch.cuda.get_rng_state(gpu_device)
+
+    monkeypatch.setattr(_graph, "ENABLED", False)
+    eager_metrics = tr.update()
+    eager = [p.detach().clone() for p in tr.params]
+
+    with torch.no_grad():
+        for p, p0 in zip(tr.params, params0):
+            p.copy_(p0)
+    for o, st in zip(opts, states0):
+        o.load_state_dict(st)
+    _graph.make_capturable(opts, tr.device)
+    tr.buffer.action_advantages[:T].copy_(adv0)
+    tr.actor_lr_scale = scale0
+    torch.cuda.set_rng_state(rng0, gpu_device)
+    tr._graphed, tr._graph_warm = None, False
+    monkeypatch.setattr(_graph, "ENABLED", True)
+    graphed_metrics = tr.update()
+    assert tr._graphed is not None and tr._graphed.replays > 0, "no step was replayed from the graph"
+
+    for k in ("actor_updates", "critic_updates", "kl_early_stop"):
+        assert graphed_metrics[k] == eager_metrics[k], k
+    worst = 0.0
+    for a, b in zip(eager, tr.params):
+        scale = a.abs().max().item() + 1e-12
+        worst = max(worst, (a - b.detach()).abs().max().item() / scale)
+    assert worst < 2e-5, worst
+    for k in ("policy_loss", "value_loss", "gradient_norm", "critic_gradient_norm", "max_policy_kl"):
+        if k in eager_metrics:
+            assert graphed_metrics[k] == pytest.approx(eager_metrics[k], rel=2e-3, abs=1e-6), k
+    print(f"[graph] oc2 target_kl={target_kl}: {tr._graphed.replays} replayed, actor updates "
+          f"{graphed_metrics['actor_updates']:.0f}/{graphed_metrics['critic_updates']:.0f}, max param diff {worst:.3g}")
+    env.close()
