@@ -54,15 +54,21 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const fl
             if (keep && j < U) k_next = keep[row + 1];
         }
         if (j < G) {
-            float a0 = 0.0f, a1 = 0.0f;
+            // four independent accumulation chains (16 deep at 64 units)
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
-            for (int k = 0; k < MAXU; k += 4)
+            for (int k = 0; k < MAXU; k += 8)
                 if (k < U) {
                     const float4 h4 = *reinterpret_cast<const float4*>(&hs[k]);
                     a0 += w[k] * h4.x + w[k + 2] * h4.z;
                     a1 += w[k + 1] * h4.y + w[k + 3] * h4.w;
+                    if (k + 4 < U) {
+                        const float4 g4 = *reinterpret_cast<const float4*>(&hs[k + 4]);
+                        a2 += w[k + 4] * g4.x + w[k + 6] * g4.z;
+                        a3 += w[k + 5] * g4.y + w[k + 7] * g4.w;
+                    }
                 }
-            const float a = (a0 + a1) + x;
+            const float a = ((a0 + a1) + (a2 + a3)) + x;
             const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
             gs[j] = v;
             act[row * G + j] = v;
