@@ -12,3 +12,8 @@ template void launch_step_m<SWARM_MISSION_ID>(const Geom&, const DevState&, cons
 template void launch_reset_m<SWARM_MISSION_ID>(const Geom&, const DevState&, const uint8_t*, const DevOut&,
                                                const DevReplay&, uint64_t, hipStream_t);
 }  // namespace swarm
+
+#if SWARM_WAVE_TIMING && SWARM_MISSION_ID == 2
+// diagnostic builds only (tools/wave_timing.py): the Homing step kernel's per-wave log
+extern "C" int swarm_debug_wave_log(void* host, size_t bytes) { return swarm::read_wave_log(host, bytes); }
+#endif

@@ -3,19 +3,20 @@
 // Device code + launch templates; swarm_mission.hip compiles it once per
 // mission (parallel translation units), swarm_dispatch.hip picks the mission.
 //
-// A workgroup holds floor(64/N) complete arenas (3 for the reference's N = 20
-// robots: lanes 0-19, 20-39, 40-59 of a wave), one robot per lane, and runs
-// W cooperating waves over those same arenas. Every wave carries the full
-// per-robot state in registers (bit-identical in all W waves); the O(N) work
-// per robot — neighbour loops of the contact solver and range-and-bearing,
-// proximity rays against walls and robots — is split into W contiguous
-// neighbour chunks / segment subsets, and the partial sums (fixed wave order)
-// or maxima are exchanged through LDS. W multiplies the waves in flight: the
-// reference workload (20 x 4096 envs) is only 1366 single waves, 1.3 per SIMD,
-// which leaves a latency-bound kernel with nothing to hide behind.
-// Positions are exchanged through a 64-entry LDS tile; per-arena integer
-// reductions (goal / target / shelter / nest counts, K+ and K-) are wave
-// ballots masked to the arena's lane range + popcount. State lives in
+// Product layout 103 (N <= 21 robots per arena): one workgroup = one wave = one
+// arena. Robot i owns the 3 adjacent lanes 3i + p (p = 0, 1, 2, its "parts"),
+// which hold bit-identical copies of its state in registers and run the O(1)
+// per-robot work redundantly. The O(N) work — contact-solver pair sums,
+// proximity rays (wall segments s = p mod 3 and the part's neighbour chunk),
+// range-and-bearing sums — is split over the 3 parts (neighbour chunks
+// [7p, 7p + 7)); partial sums (added in part order) and ray maxima are
+// exchanged through LDS inside the wave, with no barrier. The reference
+// workload (20 x 4096 envs) thereby fills 4096 waves = 4 per SIMD instead of
+// 1366 one-lane-per-robot waves. Layout 4 (four waves over floor(64/N) arenas,
+// one lane per robot per wave, cross-wave LDS combines) is the generic
+// fallback for larger N. Positions go through a 64-entry LDS tile; per-arena
+// integer reductions (goal / target / shelter / nest counts, K+ and K-) are
+// wave ballots masked to the arena's part-0 lanes + popcount. State lives in
 // registers for all substeps of a launch (the ML-Agents decision period), so
 // HBM sees each state word once per launch, the action once, and the
 // observation once per substep.
@@ -77,10 +78,34 @@
 #define SWARM_ABLATE 0
 #endif
 
+// Wave priority for arenas with live contacts (the launch's slowest waves run the
+// most solver iterations): 0 off, 1 raise to 3 at the first middle iteration that
+// moved a robot, 2 graded by the count of such iterations (1 / 2 / 3 at 3 / 6 / 9).
+#ifndef SWARM_PRIO_MODE
+#define SWARM_PRIO_MODE 0
+#endif
+
+// Diagnostic build only (tools/wave_timing.py): each wave of the production step
+// kernel records its start / end shader clock, hardware slot and work counters.
+#ifndef SWARM_WAVE_TIMING
+#define SWARM_WAVE_TIMING 0
+#endif
+
 namespace swarm {
 
 // kGeomTab[mission][profile]: compile-time copy of build_geom() (gen_tables.cpp)
 #include "swarm_geom_tables.inc"
+
+#if SWARM_WAVE_TIMING
+// per wave: {start clock lo, end - start, HW_ID, XCC_ID}, {wall start lo, wall end lo, solver passes, work}
+constexpr int kWaveLogMax = 65536;
+static __device__ uint4 g_wave_log[3 * kWaveLogMax];
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m));
+    return v;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 //  Philox4x32-10 (counter-based: results depend only on (seed, counter), so
@@ -200,7 +225,18 @@ struct Lane {
     unsigned long long amask;  // ballot bits of this arena's part-0 lanes
     int E, obs_dim;            // runtime layout (kernel argument)
     uint32_t seed_lo, seed_hi;
+#if SWARM_PRIO_MODE
+    mutable int moved_iters;   // wave-uniform count of solver iterations that moved a robot
+#endif
+#if SWARM_WAVE_TIMING
+    mutable uint32_t wt_push, wt_pair, wt_rab, wt_seg, wt_disc;   // per-lane work counters (diagnostic)
+#endif
 };
+#if SWARM_WAVE_TIMING
+#define SWARM_WT(stmt) stmt
+#else
+#define SWARM_WT(stmt)
+#endif
 
 // Philox counter (global env, robot | block << 8 | purpose << 24, tick), key = seed.
 __device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t block, uint32_t purpose,
@@ -314,6 +350,7 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 template <int LY, int C>
 __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
     if (SWARM_ABLATE & 4) return;
+    SWARM_WT(L.wt_push++);
     if (L.p == 0) S.xy[L.r] = make_float2(x, y);
     sync_wg<LY>();
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
@@ -355,6 +392,7 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
             return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
         });
         while (cand) {
+            SWARM_WT(L.wt_pair++);
             const int j = L.j0 + __builtin_ctz(cand);
             cand &= cand - 1u;
             const float2 p = S.xy[L.ab + j];
@@ -565,10 +603,25 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
             // positions (and apply's first iteration does as well), so only the
             // middle ones are skipped.
             constexpr bool middle_from0 = !INTERNAL || !apply;
-            if ((middle_from0 ? it < K : (it >= 1 && it < K)) && !__any(x != bx || y != by)) {
+            const bool middle = middle_from0 ? it < K : (it >= 1 && it < K);
+            const bool moved = __builtin_amdgcn_readfirstlane((int)__any(x != bx || y != by)) != 0;
+            if (middle && !moved) {
                 if constexpr (!INTERNAL) return;
                 fixed = true;
             }
+#if SWARM_PRIO_MODE == 1
+            if (middle && moved && L.moved_iters == 0) {
+                L.moved_iters = 1;
+                __builtin_amdgcn_s_setprio(3);
+            }
+#elif SWARM_PRIO_MODE == 2
+            if (middle && moved) {
+                const int c = ++L.moved_iters;
+                if (c == 3) __builtin_amdgcn_s_setprio(1);
+                if (c == 6) __builtin_amdgcn_s_setprio(2);
+                if (c == 9) __builtin_amdgcn_s_setprio(3);
+            }
+#endif
         }
     }
 }
@@ -660,6 +713,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     }
 #endif
     while (near_mask) {
+        SWARM_WT(L.wt_seg++);
         const int s = __builtin_ctz(near_mask);
         near_mask &= near_mask - 1u;
         const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
@@ -709,6 +763,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
         while (cand) {
+            SWARM_WT(L.wt_disc++);
             const int j = L.j0 + __builtin_ctz(cand);
             cand &= cand - 1u;
             const float2 p = S.xy[L.ab + j];
@@ -880,6 +935,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             }
         }
         while (kept) {
+            SWARM_WT(L.wt_rab++);
             const int j = L.j0 + __builtin_ctz(kept);
             kept &= kept - 1u;
             const float2 q = xy[L.ab + j];
@@ -1378,6 +1434,12 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime k
         for (int q = 0; q < L.N; ++q) m |= 1ull << (L.a * KL * L.N + q * KL);
     }
     L.amask = m;
+#if SWARM_PRIO_MODE
+    L.moved_iters = 0;
+#endif
+#if SWARM_WAVE_TIMING
+    L.wt_push = L.wt_pair = L.wt_rab = L.wt_seg = L.wt_disc = 0;
+#endif
     return L;
 }
 
@@ -1388,6 +1450,10 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     const Geom gr, const DevState st, const void* __restrict__ actions, const float* __restrict__ ovr,
     const DevOut out, const DevReplay rp_in, uint64_t tick0, int n_sub, uint64_t reset_any) {
     const DevReplay rp = REPLAY ? rp_in : DevReplay{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+#if SWARM_WAVE_TIMING
+    const uint64_t wt_c0 = __builtin_amdgcn_s_memtime();
+    const uint64_t wt_w0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const Geom& g = kGeomTab[MISSION][PROFILE];   // mission constants as literals; gr: runtime fields
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
@@ -1563,7 +1629,29 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
         }
     }
+#if SWARM_WAVE_TIMING
+    if constexpr (!REPLAY && ly_waves(LY) == 1) {
+        const uint64_t wt_c1 = __builtin_amdgcn_s_memtime();
+        const uint64_t wt_w1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+        const uint32_t push = wave_max(L.wt_push), pair = wave_max(L.wt_pair), rab = wave_max(L.wt_rab);
+        const uint32_t seg = wave_max(L.wt_seg), disc = wave_max(L.wt_disc);
+        if (threadIdx.x == 0 && blockIdx.x < kWaveLogMax) {
+            g_wave_log[3 * blockIdx.x] = make_uint4((uint32_t)wt_c0, (uint32_t)(wt_c1 - wt_c0), hw, xcc);
+            g_wave_log[3 * blockIdx.x + 1] = make_uint4((uint32_t)wt_w0, (uint32_t)wt_w1, push, pair);
+            g_wave_log[3 * blockIdx.x + 2] = make_uint4(rab, seg, disc, 0u);
+        }
+    }
+#endif
 }
+
+#if SWARM_WAVE_TIMING
+static int read_wave_log(void* host, size_t bytes) {
+    const size_t n = bytes < sizeof(g_wave_log) ? bytes : sizeof(g_wave_log);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_log), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 //  Reset kernel: _reset_idx(mask) + observations (DirectMARLEnv.reset)
