@@ -78,11 +78,24 @@
 #define SWARM_ABLATE 0
 #endif
 
-// Wave priority for arenas with live contacts (the launch's slowest waves run the
-// most solver iterations): 0 off, 1 raise to 3 at the first middle iteration that
-// moved a robot, 2 graded by the count of such iterations (1 / 2 / 3 at 3 / 6 / 9).
+// Wave priority for arenas with live contacts. A launch lasts as long as its
+// slowest wave, and the slowest waves are the arenas whose contact solver keeps
+// moving robots (up to 25 push iterations per launch against 9 on average,
+// tools/wave_timing.py). 2: graded s_setprio 1 / 2 / 3 after T / 2T / 3T solver
+// iterations that moved a robot, so those waves win the SIMD's issue
+// arbitration over co-resident waves with slack; 0: off. Scheduling only: the
+// results are bitwise the same.
 #ifndef SWARM_PRIO_MODE
-#define SWARM_PRIO_MODE 0
+#define SWARM_PRIO_MODE 2
+#endif
+#ifndef SWARM_PRIO_T
+#define SWARM_PRIO_T 2
+#endif
+
+// 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
+// correction (bitwise = sqrtf); 0: the library's sqrtf.
+#ifndef SWARM_CR_SQRT
+#define SWARM_CR_SQRT 0
 #endif
 
 // Diagnostic build only (tools/wave_timing.py): each wave of the production step
@@ -175,6 +188,21 @@ __device__ __forceinline__ float u01_of5(const uint4& r, int w) {
 // overlap, RAB range, line of sight) keep IEEE division / sqrt.
 __device__ __forceinline__ float frcp(float v) { return __builtin_amdgcn_rcpf(v); }
 __device__ __forceinline__ float fsqrt(float v) { return __builtin_amdgcn_sqrtf(v); }
+// Correctly rounded sqrt (bitwise = sqrtf) for arguments known to be positive,
+// finite and normal (here sums of squares + 1e-8 or 1e-6): the hardware result
+// moved by one ulp where the residual says so, without the library
+// expansion's denormal scaling and inf / zero class fix-ups.
+__device__ __forceinline__ float nsqrt(float v) {
+#if SWARM_CR_SQRT
+    const float r = __builtin_amdgcn_sqrtf(v);
+    const float dn = __uint_as_float(__float_as_uint(r) - 1u), up = __uint_as_float(__float_as_uint(r) + 1u);
+    float o = fmaf(-dn, r, v) <= 0.0f ? dn : r;
+    o = fmaf(-up, r, v) > 0.0f ? up : o;
+    return o;
+#else
+    return sqrtf(v);
+#endif
+}
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
@@ -270,6 +298,16 @@ __device__ __forceinline__ void sync_wg() {
     }
 }
 
+#if SWARM_PRIO_MODE == 2
+// one more unit of wave-uniform work seen: raise the priority at T, 2T, 3T units
+__device__ __forceinline__ void prio_bump(const Lane& L) {
+    const int c = ++L.moved_iters;
+    if (c == SWARM_PRIO_T) __builtin_amdgcn_s_setprio(1);
+    if (c == 2 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(2);
+    if (c == 3 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(3);
+}
+#endif
+
 __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     const unsigned long long m = __ballot(pred);
     return __popcll(m & L.amask);
@@ -357,7 +395,7 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
     auto pair_term = [&](int j, float dx, float dy) {
-        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
         const float ov = g.min_dist - dist;
         if (!(ov > 0.0f)) return;
         const float inv = frcp(dist + 1e-8f);
@@ -609,18 +647,8 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
                 if constexpr (!INTERNAL) return;
                 fixed = true;
             }
-#if SWARM_PRIO_MODE == 1
-            if (middle && moved && L.moved_iters == 0) {
-                L.moved_iters = 1;
-                __builtin_amdgcn_s_setprio(3);
-            }
-#elif SWARM_PRIO_MODE == 2
-            if (middle && moved) {
-                const int c = ++L.moved_iters;
-                if (c == 3) __builtin_amdgcn_s_setprio(1);
-                if (c == 6) __builtin_amdgcn_s_setprio(2);
-                if (c == 9) __builtin_amdgcn_s_setprio(3);
-            }
+#if SWARM_PRIO_MODE == 2
+            if (middle && moved) prio_bump(L);
 #endif
         }
     }
@@ -814,7 +842,7 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
         return;
     }
     const float lx = g.light_x - x, ly = g.light_y - y;
-    const float dist = sqrtf(lx * lx + ly * ly + 1e-6f);
+    const float dist = nsqrt(lx * lx + ly * ly + 1e-6f);
     const float base = g.light_int * frcp(dist * g.inv_unity);
     const float il = frcp(dist + 1e-8f);
     const float nlx = lx * il, nly = ly * il;
@@ -851,7 +879,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
     ayy = 0.0f;
     // one kept, in-range neighbour (exact distance test, LOS, bearing terms)
     auto term = [&](int j, float dx, float dy) {
-        const float dist = sqrtf(dx * dx + dy * dy + 1e-8f);
+        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
         if (!(dist < g.rab_range)) return;
         // line of sight (ES:462-501): arena faces can only block if an end point is
         // not strictly inside the convex arena; internal walls are always tested.
