@@ -95,7 +95,7 @@
 // 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
 // correction (bitwise = sqrtf); 0: the library's sqrtf.
 #ifndef SWARM_CR_SQRT
-#define SWARM_CR_SQRT 0
+#define SWARM_CR_SQRT 1
 #endif
 
 // Diagnostic build only (tools/wave_timing.py): each wave of the production step
