@@ -233,22 +233,25 @@ def main():
         eng.step(acts[d], dp, out=out)
     torch.cuda.synchronize(dev)
 
+    # HIP events on the launch stream bracket the whole timed region (not every launch:
+    # each event is a packet of its own in the stream, and a pair per decision added
+    # ~5 us of GPU-side gap per launch); the per-launch average includes the gaps between
+    # back-to-back launches, so it is an upper bound on the kernel's own duration.
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_dec)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for d in range(n_dec):
-        ev[d][0].record(stream)
         eng.step(acts[n_warm + d], dp, out=out)
-        ev[d][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    avg_kernel_s = ev0.elapsed_time(ev1) / n_dec / 1e3
     elapsed = max_over_ranks(elapsed, dev)
     total_agent_steps = world * E * N_AGENTS * steps
     value = total_agent_steps / elapsed
