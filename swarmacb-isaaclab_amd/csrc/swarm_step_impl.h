@@ -91,11 +91,6 @@
 #ifndef SWARM_PRIO_T
 #define SWARM_PRIO_T 2
 #endif
-// 1: an arena whose solver reaches a fixed point at its first iteration (no contact
-// left) steps its priority down one level
-#ifndef SWARM_PRIO_DECAY
-#define SWARM_PRIO_DECAY 0
-#endif
 
 // 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
 // correction (bitwise = sqrtf); 0: the library's sqrtf.
@@ -310,15 +305,6 @@ __device__ __forceinline__ void prio_bump(const Lane& L) {
     if (c == SWARM_PRIO_T) __builtin_amdgcn_s_setprio(1);
     if (c == 2 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(2);
     if (c == 3 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(3);
-}
-// no contact in this substep: one priority level down
-__device__ __forceinline__ void prio_decay(const Lane& L) {
-    const int lv = min(L.moved_iters / SWARM_PRIO_T, 3);
-    if (lv == 0) return;
-    L.moved_iters = (lv - 1) * SWARM_PRIO_T;
-    if (lv == 1) __builtin_amdgcn_s_setprio(0);
-    if (lv == 2) __builtin_amdgcn_s_setprio(1);
-    if (lv == 3) __builtin_amdgcn_s_setprio(2);
 }
 #endif
 
@@ -658,9 +644,6 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
             const bool middle = middle_from0 ? it < K : (it >= 1 && it < K);
             const bool moved = __builtin_amdgcn_readfirstlane((int)__any(x != bx || y != by)) != 0;
             if (middle && !moved) {
-#if SWARM_PRIO_MODE == 2 && SWARM_PRIO_DECAY
-                if (it == 0) prio_decay(L);
-#endif
                 if constexpr (!INTERNAL) return;
                 fixed = true;
             }
