@@ -83,11 +83,15 @@ class TrainerBase:
         self.device = torch.device(self.unwrapped.device)
         self.comm = TrainerComm(group)
         self.num_envs = self.unwrapped.scene.num_envs
+        # agent-decisions per decision over ALL ranks: the shards may differ by one env
+        # (shard.EnvShard), so every rank counts the global sum, never local * world
+        self.global_num_envs = self.comm.sum_int(self.num_envs)
         cfg_env = self.unwrapped.cfg
         self.num_agents = getattr(cfg_env, "num_agents", getattr(cfg_env, "num_robots", None))
         self.discrete = bool(getattr(cfg_env, "discrete_actions", False))
         self.variant = getattr(cfg_env, "variant", None)
         self.agents = list(cfg_env.possible_agents)
+        self.per_decision = self.global_num_envs * self.num_agents
         sample = self.env.reset()[0][self.agents[0]]
         self.obs_dim = int(sample[0].numel()) if sample.ndim == 4 else int(sample.shape[1])
         self.state_dim = 5
@@ -118,7 +122,7 @@ class TrainerBase:
     def _buffer_capacity(self) -> int:
         """horizon + the decisions the ML-Agents trigger may add, counted over ALL ranks
         (poca_trainer.py:337-340, option_critic_trainer.py:207-210)."""
-        per_decision = self.num_envs * self.num_agents * self.comm.world
+        per_decision = self.per_decision
         return self.cfg.horizon + (self.cfg.buffer_size_hint + per_decision - 1) // per_decision + 1
 
     def _apply_schedules(self):
@@ -192,7 +196,7 @@ class TrainerBase:
         (poca_trainer.py:882-908, option_critic_trainer.py:786-814)."""
         c = self.cfg
         self.buffer.reset()
-        per = self.num_envs * self.num_agents * self.comm.world
+        per = self.per_decision
         while self.global_step < c.total_timesteps:
             remaining = c.total_timesteps - self.global_step
             remaining_steps = max(1, (remaining + per - 1) // per)
@@ -273,6 +277,13 @@ class TrainerBase:
                 self._manage_checkpoints(ckpt_dir)
         if pbar is not None:
             pbar.close()
+        # every rank must end with rank 0's parameters (one global update per step)
+        self.comm.assert_replicated(self.params, "parameters after training")
+        if self.comm.active:
+            d = self.comm._digest(self.params).tolist()
+            print(f"[{self.algo}] rank {self.comm.rank}/{self.comm.world}: envs {self.num_envs} of "
+                  f"{self.global_num_envs}, updates {self.update_count}, step {self.global_step}, "
+                  f"parameter digest {d[0]}:{d[1]} (bitwise equal on every rank)", flush=True)
         self.writer.close()
         self.save_checkpoint(ckpt_dir / f"{self.ckpt_prefix}_final.pt")
         elapsed = time.time() - start_time
@@ -293,7 +304,8 @@ class TrainerBase:
         replaced optimizer tensors, so it is dropped (the next update recaptures)."""
         self._graphed = None
         if self.comm.flat_grad is not None:   # optimizer state loaded; keep grads bound to the flat buffer
-            self.comm.bind_flat_grads(self.params)
+            self.comm.bind_flat_grads(self.params)           # also re-syncs the parameters from rank 0
+            self.comm.sync_optimizer_state(self.optimizer, "optimizer state after resume")
 
     def _manage_checkpoints(self, ckpt_dir: Path):
         """Keep the keep_checkpoints most recent numbered checkpoints (poca_trainer.py:1109-1123)."""

@@ -246,7 +246,11 @@ def evaluate(env, actor, num_episodes: int, decision_period: int, deterministic:
     while count < num_episodes:
         flat_obs = torch.stack([obs_dict[a] for a in agents], dim=1).reshape(E * N, -1)
         all_actions = policy.act(flat_obs)
-        action_dict = {a: all_actions[:, i].clone() for i, a in enumerate(agents)}
+        # views, as in play.py:640-641: for the fixed-option kind all_actions IS a view of
+        # the current options, so zeroing a finished env's actions below (play.py:703)
+        # also turns its freshly reset option (-1, play.py:689) into option 0 — the
+        # reference's effective semantics, reproduced rather than "fixed"
+        action_dict = {a: all_actions[:, i] for i, a in enumerate(agents)}
         active = torch.ones(E, dtype=torch.bool, device=dev)
         for _ in range(decision_period):
             obs_dict, rew, term, trunc, _ = env.step(action_dict)

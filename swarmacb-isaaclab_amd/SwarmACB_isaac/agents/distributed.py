@@ -99,12 +99,76 @@ class TrainerComm:
         adv.copy_(((adv - mean.float()) / (std.float() + eps)))
         return adv
 
+    # ------------------------------------------------------------ replication
+    def _src(self) -> int:
+        """Global rank of the group's rank 0 (the broadcast source)."""
+        return 0 if self.group is None else self.dist.get_global_rank(self.group, 0)
+
+    def broadcast_(self, tensors) -> None:
+        """Overwrite every tensor with rank 0's values, in place (multi-rank only)."""
+        if not self.active:
+            return
+        for t in tensors:
+            x = t.detach()
+            dev_ok = (self.backend == "gloo") == (x.device.type == "cpu")
+            y = x if dev_ok else x.to(self._dev())
+            if not y.is_contiguous():
+                y = y.contiguous()
+            self.dist.broadcast(y, src=self._src(), group=self.group)
+            if y is not x:
+                x.copy_(y)
+
+    @staticmethod
+    def _digest(tensors) -> torch.Tensor:
+        """Bit-level digest of a tensor list: (Σ bits, Σ bits·position) of the int32 words,
+        in int64 on the host; differs when any element differs in any bit (up to collisions)."""
+        acc = torch.zeros(2, dtype=torch.int64)
+        pos = 1
+        for t in tensors:
+            x = t.detach().contiguous().reshape(-1)
+            if x.dtype.itemsize != 4:
+                x = x.to(torch.float32) if x.is_floating_point() else x.to(torch.int32)
+            w = x.view(torch.int32).to(torch.int64).cpu()
+            idx = torch.arange(pos, pos + w.numel(), dtype=torch.int64)
+            acc[0] += w.sum()
+            acc[1] += (w * idx).sum()
+            pos += w.numel()
+        return acc
+
+    def assert_replicated(self, tensors, what: str) -> None:
+        """Raise unless every rank holds bitwise the same tensors (one 2-int all-reduce each of max / min)."""
+        if not self.active:
+            return
+        tensors = list(tensors)
+        d = self._digest(tensors).to(self._dev())
+        hi, lo = d.clone(), d.clone()
+        self._reduce(hi, "max")
+        self._reduce(lo, "min")
+        if not torch.equal(hi, lo):
+            raise RuntimeError(f"{what} differ between the ranks of the training group (rank {self.rank})")
+
+    def sync_module_state(self, tensors, what: str) -> None:
+        """Rank 0's values on every rank, then a bitwise check."""
+        tensors = list(tensors)
+        self.broadcast_(tensors)
+        self.assert_replicated(tensors, what)
+
+    def sync_optimizer_state(self, optimizer, what: str = "optimizer state") -> None:
+        """Broadcast every tensor of an optimizer's state (Adam moments, step counts) from rank 0."""
+        if not self.active:
+            return
+        ts = [v for st in optimizer.state.values() for v in st.values() if torch.is_tensor(v)]
+        self.sync_module_state(ts, what)
+
     # ------------------------------------------------------------ gradients
     def bind_flat_grads(self, params) -> torch.Tensor | None:
-        """Back every parameter's .grad by a view of one flat fp32 buffer (multi-rank only)."""
+        """Back every parameter's .grad by a view of one flat fp32 buffer (multi-rank only).
+        The parameters themselves are made identical on every rank first (rank 0's
+        values, checked bitwise): ranks must not rely on seeding alike."""
         self._params = [p for p in params if p.requires_grad]
         if not self.active or not self._params:
             return None
+        self.sync_module_state(self._params, "initial parameters")
         dev = self._params[0].device
         n = sum(p.numel() for p in self._params)
         self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)

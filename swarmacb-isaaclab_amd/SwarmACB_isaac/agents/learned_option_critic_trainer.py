@@ -268,7 +268,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         t0 = time.perf_counter()
         nxt = self.collector.collect(stack_obs(obs_dict, self.agents), steps, reset_buffer=reset_buffer)
         self._rollout_seconds += time.perf_counter() - t0
-        self.global_step += self.num_envs * self.num_agents * self.comm.world * steps
+        self.global_step += self.per_decision * steps
         return {a: nxt[:, i] for i, a in enumerate(self.agents)}
 
     def _on_train_start(self):
@@ -573,6 +573,22 @@ class LearnedOptionCriticTrainer(TrainerBase):
         step = self._step_runner(self._oc2_step, [self.actor_optimizer, self.critic_optimizer])
         key = (self.current_eps, self.current_beta, self.current_lr, self.current_actor_lr,
                self.current_termination_prior_coef, self.current_option_balance_coef)
+        # The eager path (and the reference) raise BEFORE an optimizer step takes a bad
+        # minibatch; replayed steps are checked only after the last one. Keep the
+        # update-start parameters and Adam state (a few MB on the device): a failed check
+        # restores them, so no step taken on non-finite values survives the exception.
+        opts = (self.actor_optimizer, self.critic_optimizer)
+        live = list(self.actor_parameters) + list(self.critic_parameters) + \
+            [v for o in opts for st in o.state.values() for v in st.values() if torch.is_tensor(v)]
+        with torch.no_grad():
+            saved = [t.detach().clone() for t in live]
+
+        def fail(exc):
+            with torch.no_grad():
+                for t, b in zip(live, saved):
+                    t.copy_(b)
+            raise exc
+
         for _epoch in range(cfg.num_epochs):
             for batch in self._sequence_batches():
                 step(batch, key)
@@ -584,18 +600,18 @@ class LearnedOptionCriticTrainer(TrainerBase):
         actor_early_stopped = bool(host[6])
         bad = host[7:11]
         if num_batches and initial_policy_kl > 1e-6:
-            raise RuntimeError(f"OC2 update-start policy does not match its frozen reference "
-                               f"(KL={initial_policy_kl:.6g}).")
+            fail(RuntimeError(f"OC2 update-start policy does not match its frozen reference "
+                              f"(KL={initial_policy_kl:.6g})."))
         for flag, which in ((bad[0], "actor loss"), (bad[1], "critic loss"), (bad[2], "actor gradient"),
                             (bad[3], "critic gradient")):
             if flag:
-                raise FloatingPointError(f"LearnedOC produced a non-finite {which} during the update")
+                fail(FloatingPointError(f"LearnedOC produced a non-finite {which} during the update"))
         if actor_early_stopped and self.comm.rank == 0:
             print(f"[LearnedOC] Actor PPO early stop: policy KL exceeded {1.5 * cfg.target_kl:.4f}; "
                   f"centralized critics continue")
         if actor_updates == 0:
-            raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
-                               "should guarantee at least one safe policy minibatch.")
+            fail(RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
+                              "should guarantee at least one safe policy minibatch."))
         return G["totals"].clone(), G["grad_norms"].clone(), G["samples"].clone(), num_batches, actor_updates, \
             num_batches, max_policy_kl, max_action_kl, max_option_kl, initial_policy_kl, actor_early_stopped
 
@@ -938,6 +954,8 @@ class LearnedOptionCriticTrainer(TrainerBase):
         if self.actor_comm.flat_grad is not None:
             self.actor_comm.bind_flat_grads(self.actor_parameters)
             self.critic_comm.bind_flat_grads(self.critic_parameters)
+            self.actor_comm.sync_optimizer_state(self.actor_optimizer, "actor optimizer state after resume")
+            self.critic_comm.sync_optimizer_state(self.critic_optimizer, "critic optimizer state after resume")
         self.global_step = int(ck["global_step"])
         self.update_count = int(ck["update_count"])
         self.actor_lr_scale = float(ck.get("actor_lr_scale", 1.0))

@@ -105,7 +105,7 @@ class FixedOptionCriticTrainer(TrainerBase):
 
         steps = self.cfg.horizon if rollout_steps is None else int(rollout_steps)
         nxt = self.collector.collect(stack_obs(obs_dict, self.agents), steps, reset_buffer=reset_buffer)
-        self.global_step += self.num_envs * self.num_agents * self.comm.world * steps
+        self.global_step += self.per_decision * steps
         return {a: nxt[:, i] for i, a in enumerate(self.agents)}
 
     def _on_train_start(self):

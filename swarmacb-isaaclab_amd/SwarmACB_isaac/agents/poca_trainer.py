@@ -113,7 +113,7 @@ class POCATrainer(TrainerBase):
         steps = self.cfg.horizon if rollout_steps is None else int(rollout_steps)
         obs = _stack_obs(obs_dict, self.agents)
         nxt = self.collector.collect(obs, steps, reset_buffer=reset_buffer)
-        self.global_step += self.num_envs * self.num_agents * self.comm.world * steps
+        self.global_step += self.per_decision * steps
         return {a: nxt[:, i] for i, a in enumerate(self.agents)}
 
     # ------------------------------------------------------------ losses

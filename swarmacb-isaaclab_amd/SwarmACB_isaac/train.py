@@ -116,10 +116,13 @@ def main(argv=None) -> int:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if device.type == "cuda":
+        # RCCL over xGMI on GPUs; SWARM_DIST_BACKEND=gloo rehearses the same collectives
+        # over TCP (e.g. several ranks sharing one GPU, which RCCL refuses)
+        backend = os.environ.get("SWARM_DIST_BACKEND", "nccl" if device.type == "cuda" else "gloo")
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group(backend)
 
     run_name, variant, cfg, env_overrides, task_id = resolve(args)
     random.seed(cfg.seed)
@@ -132,15 +135,15 @@ def main(argv=None) -> int:
 
     trainer_type = getattr(cfg, "trainer_type", "poca")
     env_cfg = make_env_cfg(task_id, variant, env_overrides, trainer_type, seed=cfg.seed)
-    shard = EnvShard(int(env_cfg.scene.num_envs) * 1, rank, world) if world > 1 else None
+    shard = EnvShard(int(env_cfg.scene.num_envs), rank, world) if world > 1 else None
     if shard is not None:
         env_cfg.scene.num_envs = shard.local_envs
         env_cfg.env_offset = shard.env_offset
     env = make(task_id, env_cfg, device=device)
     trainer = make_trainer(env, cfg)
     if world > 1:
-        # identical initial weights on every rank (same seed above); independent action
-        # sampling per rank from here on
+        # the trainer broadcast rank 0's initial weights and checked them bitwise
+        # (TrainerComm.bind_flat_grads); independent action sampling per rank from here on
         torch.manual_seed(cfg.seed + 7919 * rank)
     if args.checkpoint:
         trainer.load_checkpoint(args.checkpoint)

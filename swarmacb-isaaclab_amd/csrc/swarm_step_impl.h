@@ -385,9 +385,11 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 
 // DG:1080-1112 / MC:555-571 — Jacobi half-overlap push over pairs i<j.
 // Each wave sums its neighbour chunk; the W partial sums are added in wave order.
+// Returns false only when it is known (wave-uniformly) that no pair term
+// contributed, i.e. the push was the identity map on every lane.
 template <int LY, int C>
-__device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
-    if (SWARM_ABLATE & 4) return;
+__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
+    if (SWARM_ABLATE & 4) return false;
     SWARM_WT(L.wt_push++);
     if (L.p == 0) S.xy[L.r] = make_float2(x, y);
     sync_wg<LY>();
@@ -461,7 +463,7 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
             if (!__any(rx != 0.0f || ry != 0.0f || cx != 0.0f || cy != 0.0f)) {
                 x = (x + 0.0f) - 0.0f;
                 y = (y + 0.0f) - 0.0f;
-                return;
+                return false;
             }
         }
         S.red[0][L.tid] = make_float4(rx, ry, cx, cy);
@@ -484,6 +486,7 @@ __device__ __forceinline__ void robots_push(const Geom& g, const Lane& L, Shared
     }
     x = (x + rx) - cx;
     y = (y + ry) - cy;
+    return true;
 }
 
 // DG:658-705 (DirGate and XOR, which keeps the base-class version)
@@ -620,7 +623,8 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     for (int it = 0; it <= K; ++it) {
         if (fixed && it < K) continue;
         const float bx = x, by = y;
-        if (it < K) robots_push<LY, C>(g, L, S, x, y);
+        bool pushed = false;
+        if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
@@ -636,15 +640,19 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
         if constexpr (ly_waves(LY) == 1 && SWARM_SOLVE_SHORTCUTS) {
             // Fixed point: if no robot of the wave's arenas moved in a middle
             // iteration, every later middle iteration (same body) maps the same
-            // positions to themselves. Without internal walls the last iteration
-            // (no push) is a no-op too; with internal walls it uses the pre-step
-            // positions (and apply's first iteration does as well), so only the
-            // middle ones are skipped.
+            // positions to themselves. The last iteration (no push) is a no-op
+            // too only if the push itself contributed nothing (then walls and gate
+            // alone kept x; a push exactly undone by a wall would not prove that),
+            // and without internal walls: with them it uses the pre-step positions
+            // (and apply's first iteration does as well), so only the middle ones
+            // are skipped.
             constexpr bool middle_from0 = !INTERNAL || !apply;
             const bool middle = middle_from0 ? it < K : (it >= 1 && it < K);
             const bool moved = __builtin_amdgcn_readfirstlane((int)__any(x != bx || y != by)) != 0;
             if (middle && !moved) {
-                if constexpr (!INTERNAL) return;
+                if constexpr (!INTERNAL) {
+                    if (!pushed) return;
+                }
                 fixed = true;
             }
 #if SWARM_PRIO_MODE == 2

@@ -3,28 +3,37 @@
 Tolerance (stated once, used by every parity test):
   * integer / discrete outputs (FSM states and counters, rewards as counts,
     episode counters, truncation, ground codes): exact;
-  * fp32 outputs: |got - ref| <= 1e-5 * scale + 4 * min(spread, 1e-2), where
-    `scale` = max(1, |ref|) — for the range-and-bearing projections (obs
-    channels 20-23 of the 24-D observation) and the attraction vector (sensor
-    cache rows 4-5) the magnitude of the vector they project (a component of a
-    sum of up to 19 bearing terms is as accurate as the sum, not as its own
-    value) — and `spread` is how far the oracle's own output moves when its
-    inputs are perturbed by one ulp (yaw +-1 ulp, positions +-1 ulp) or when
-    every cos/sin/atan2/exp result inside the step is nudged by +-1 ulp. The
+  * fp32 outputs: |got - ref| <= 1e-5 * scale + 4 * spread, where `scale` =
+    max(1, |ref|) — for the range-and-bearing projections (obs channels 20-23
+    of the 24-D observation) and the attraction vector (sensor cache rows 4-5)
+    the magnitude of the vector they project (a component of a sum of up to 19
+    bearing terms is as accurate as the sum, not as its own value) — and
+    `spread` is how far the oracle's own output moves when its inputs are
+    perturbed by one ulp (yaw +-1 ulp, positions +-1 ulp) or when every
+    cos/sin/atan2/exp result inside the step is nudged by +-1 ulp. The
     reference evaluates those with SLEEF on the CPU; any other implementation
     (glibc here, ocml on the GPU) differs by about 1 ulp, and near-tangent IR
     rays (ray-disc hits with r^2 - c^2 ~ 1e-7) / near-perpendicular light
     sensors amplify that by 10^2-10^3. The spread term is zero for
-    well-conditioned elements, so for them the bar is the plain 1e-5. It is
-    capped at 1e-2: an element that only a larger envelope would pass fails.
+    well-conditioned elements, so for them the bar is the plain 1e-5. The
+    spread is capped at SPREAD_CAP = 1e-3 in this rule.
+  * ill-conditioned elements (spread > SPREAD_CAP: a discontinuity or a square
+    root singularity lies within one ulp of the inputs, e.g. an IR ray tangent
+    to a robot disc, whose reading jumps from 0 to 1 - proj/0.1 at tangency)
+    may pass the rule above, or else only if BOTH compared values lie inside
+    the hull of the oracle's own outputs under the perturbations, widened by
+    the plain 1e-5 bar: either value is then an outcome the reference's
+    arithmetic itself reaches one ulp away. Every such element is recorded
+    (`hull_elements` and the first few listed in `hull_examples`).
   * angles (yaw, the proximity / light angles of the sensor cache) are compared
     modulo 2*pi, and their spread is measured modulo 2*pi: yaw = atan2(sin, cos)
     (DG:826) maps a heading at +-pi to either end, both correct.
   * A discrete output may differ only where a 1-ulp perturbation of the
     oracle's inputs also changes it (a threshold sits within rounding).
   * `compare(..., stats=d)` counts the fp32 elements that pass only through the
-    envelope and the discrete elements exempted as unstable, so every test can
-    report how much of its verdict rests on the envelope.
+    envelope (and the largest |delta| among them, per key), the hull elements
+    and the discrete elements exempted as unstable, so every test can report how
+    much of its verdict rests on the envelope.
 """
 
 from __future__ import annotations
@@ -39,7 +48,8 @@ from oracle import oracle as O
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 RTOL = 1e-5
 SPREAD_FACTOR = 4.0
-SPREAD_CAP = 1e-2
+SPREAD_CAP = 1e-3
+HULL_EXAMPLES = 8
 TWO_PI = 2.0 * np.pi
 
 FLOAT_KEYS = ("obs", "pos", "yaw", "cache", "terminal_critic", "wheel_l", "wheel_r", "ep_reward",
@@ -66,6 +76,19 @@ def _delta(key: str, a, b) -> np.ndarray:
     if m is not None:
         d = np.where(m, np.minimum(d, np.abs(d - TWO_PI)), d)
     return d
+
+
+def _signed(key: str, a, b) -> np.ndarray:
+    """a - b in float64, wrapped into (-pi, pi] on angle elements."""
+    d = np.asarray(a, np.float64) - np.asarray(b, np.float64)
+    m = _angle_mask(key, d.shape)
+    if m is not None:
+        d = np.where(m, d - TWO_PI * np.round(d / TWO_PI), d)
+    return d
+
+
+def _base_key(k: str) -> str:
+    return k.split("@", 1)[0]
 
 
 def _scale(key: str, r: np.ndarray) -> np.ndarray:
@@ -155,6 +178,11 @@ def accumulate_spread(spread: dict, out: dict, base: dict) -> dict:
             continue
         if k in FLOAT_KEYS:
             spread[k] = np.maximum(spread.get(k, 0.0), _delta(k, v, base[k]))
+            # hull of the outputs, as signed offsets from the base (angles wrapped)
+            sd = _signed(k, v, base[k])
+            spread[k + "@lo"] = np.minimum(spread.get(k + "@lo", 0.0), sd)
+            spread[k + "@hi"] = np.maximum(spread.get(k + "@hi", 0.0), sd)
+            spread[k + "@base"] = np.asarray(base[k], np.float64)
         else:
             spread[k] = spread.get(k, np.zeros(np.shape(v), bool)) | (np.asarray(v) != np.asarray(base[k]))
     return spread
@@ -165,14 +193,41 @@ def tolerance(key: str, r: np.ndarray, spread) -> np.ndarray:
     return RTOL * _scale(key, r) + SPREAD_FACTOR * sp
 
 
+def _in_hull(key: str, v, spread: dict, plain) -> np.ndarray:
+    """v inside [base + lo, base + hi] widened by `plain` (angles modulo 2 pi)."""
+    base = spread[key + "@base"]
+    off = _signed(key, v, base)
+    return (off >= spread[key + "@lo"] - plain) & (off <= spread[key + "@hi"] + plain)
+
+
+def float_verdict(key: str, g, r, spread: dict | None):
+    """(ok, plain_ok, hull_only) element masks of the fp32 rule in the module docstring."""
+    d = _delta(key, g, r)
+    plain = RTOL * _scale(key, r)
+    sp = None if spread is None else spread.get(key, 0.0)
+    plain_ok = d <= plain
+    ok = d <= tolerance(key, r, sp)
+    hull_only = np.zeros(d.shape, bool)
+    if spread is not None and (key + "@base") in spread:
+        ill = np.broadcast_to(np.asarray(sp), d.shape) > SPREAD_CAP
+        cand = ill & ~ok
+        if cand.any():
+            hull_only = cand & _in_hull(key, g, spread, plain) & _in_hull(key, r, spread, plain)
+            ok = ok | hull_only
+    return ok, plain_ok, hull_only
+
+
 def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = None) -> list[str]:
     """Return a list of human-readable violations (empty = parity holds). With
     `stats`, add the envelope counts (see the module docstring)."""
     errors = []
     keys = keys if keys is not None else [k for k in ref if k in got]
     if stats is not None:
-        for c in ("elements", "spread_only_elements", "discrete_exempt_elements", "spread_capped_elements"):
+        for c in ("elements", "spread_only_elements", "discrete_exempt_elements", "spread_capped_elements",
+                  "hull_elements"):
             stats.setdefault(c, 0)
+        stats.setdefault("envelope_max_delta", {})
+        stats.setdefault("hull_examples", [])
     for k in keys:
         if k not in got or k not in ref:
             continue
@@ -181,17 +236,29 @@ def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = 
         if g.shape != r.shape:
             g = g.reshape(r.shape)
         if k in FLOAT_KEYS:
-            d = _delta(k, g, r)
-            sp = spread.get(k, 0.0)
-            tol = tolerance(k, r, sp)
-            bad = ~(d <= tol)
+            ok, plain, hull_only = float_verdict(k, g, r, spread)
+            bad = ~ok
             if stats is not None:
-                plain = d <= RTOL * _scale(k, r)
-                stats["elements"] += int(d.size)
-                stats["spread_only_elements"] += int((~plain & ~bad).sum())
-                stats["spread_capped_elements"] += int((np.broadcast_to(np.asarray(sp), d.shape) > SPREAD_CAP).sum())
+                sp = np.broadcast_to(np.asarray(spread.get(k, 0.0)), ok.shape)
+                env_only = ~plain & ok
+                stats["elements"] += int(ok.size)
+                stats["spread_only_elements"] += int((env_only & ~hull_only).sum())
+                stats["hull_elements"] += int(hull_only.sum())
+                stats["spread_capped_elements"] += int((sp > SPREAD_CAP).sum())
+                cont_only = env_only & ~hull_only
+                if cont_only.any():
+                    dmax = float(_delta(k, g, r)[cont_only].max())
+                    stats["envelope_max_delta"][k] = max(stats["envelope_max_delta"].get(k, 0.0), dmax)
+                for idx in np.argwhere(hull_only)[:max(0, HULL_EXAMPLES - len(stats["hull_examples"]))]:
+                    idx = tuple(int(i) for i in idx)
+                    b = spread[k + "@base"][idx]
+                    stats["hull_examples"].append(
+                        {"key": k, "index": list(idx), "got": float(g[idx]), "ref": float(r[idx]),
+                         "hull": [float(b + spread[k + "@lo"][idx]), float(b + spread[k + "@hi"][idx])],
+                         "spread": float(sp[idx])})
             if bad.any():
                 idx = tuple(np.argwhere(bad)[0])
+                tol = tolerance(k, r, spread.get(k, 0.0))
                 errors.append(f"{k}: {int(bad.sum())} elems beyond tol; e.g. {idx} got {g[idx]!r} ref {r[idx]!r} "
                               f"tol {float(np.broadcast_to(tol, bad.shape)[idx]):.3g}")
         else:
@@ -205,6 +272,24 @@ def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = 
                 idx = tuple(np.argwhere(hard)[0])
                 errors.append(f"{k}: {int(hard.sum())} mismatches; e.g. {idx} got {g[idx]!r} ref {r[idx]!r}")
     return errors
+
+
+def merge_stats(stats_list: list[dict]) -> dict:
+    """Totals of several `compare` / `check_kernel_step` stats: counts add up, the per-key
+    maxima take the max, the hull examples are concatenated (first HULL_EXAMPLES)."""
+    tot: dict = {}
+    for st in stats_list:
+        for k, v in st.items():
+            if isinstance(v, dict):
+                d = tot.setdefault(k, {})
+                for kk, vv in v.items():
+                    d[kk] = max(d.get(kk, 0.0), vv)
+            elif isinstance(v, list):
+                lst = tot.setdefault(k, [])
+                lst += v[:max(0, HULL_EXAMPLES - len(lst))]
+            else:
+                tot[k] = tot.get(k, 0) + v
+    return tot
 
 
 def record_stats(test: str, stats: dict):
@@ -233,7 +318,7 @@ def _take_envs(d: dict, envs, axes: dict, default_axis=0, skip=()):
         if k in skip or not isinstance(v, np.ndarray) or v.ndim == 0:
             out[k] = v
             continue
-        out[k] = np.ascontiguousarray(np.take(v, envs, axis=axes.get(k, default_axis)))
+        out[k] = np.ascontiguousarray(np.take(v, envs, axis=axes.get(_base_key(k), default_axis)))
     return out
 
 
@@ -246,7 +331,7 @@ def _bad_envs(got: dict, ref: dict, spread: dict | None, E: int, keys=None) -> n
         r = np.asarray(ref[k])
         g = np.asarray(got[k]).reshape(r.shape)
         if k in FLOAT_KEYS:
-            bad = ~(_delta(k, g, r) <= tolerance(k, r, None if spread is None else spread.get(k, 0.0)))
+            bad = ~float_verdict(k, g, r, spread)[0]
         else:
             bad = g != r
             if spread is not None:
@@ -315,7 +400,8 @@ def check_kernel_step(cfg: tuple, before: dict, actions, draws: dict, got: dict)
     ref = run(None)
     stats = {"elements": int(sum(np.asarray(v).size for k, v in ref.items() if k in got)),
              "envs_needing_envelope": 0, "spread_only_elements": 0, "discrete_exempt_elements": 0,
-             "spread_capped_elements": 0, "envs_sensor_stage": 0}
+             "spread_capped_elements": 0, "hull_elements": 0, "envs_sensor_stage": 0,
+             "envelope_max_delta": {}, "hull_examples": []}
     bad = _bad_envs(got, ref, None, E)
     if not bad.any():
         return [], stats

@@ -24,7 +24,7 @@ SPAWN_K = 16   # rejection attempts regenerated for the oracle (acceptance >= 0.
 
 
 def _report(name, stats_list):
-    tot = {k: sum(s.get(k, 0) for s in stats_list) for k in stats_list[0]}
+    tot = parity.merge_stats(stats_list)
     parity.record_stats(f"gpu_philox/{name}", tot)
     return tot
 
@@ -103,6 +103,50 @@ def test_production_kernel_vs_oracle(name, mission, E, obs_dim, discrete, max_le
     cfg = (mission, "isaac", E, 20, obs_dim, discrete, max_len)
     stats, n_to = _teacher_forced(eng, cfg, lambda k: acts[k // 5], 50, seed, tag=name)
     eng.close()
+    assert n_to >= 10 + 7 + 1 + 40
+    _report(name, stats)
+
+
+def _config_engine(env_cls, variant, E, seed, gpu_device, continuous_full_obs=False):
+    """The env exactly as a config builds it (registry cfg class, update_variant,
+    use_continuous_actions for the learned-option phase 2, DGC:184-209)."""
+    cfg = env_cls.cfg_class()
+    cfg.update_variant(variant)
+    if continuous_full_obs:
+        cfg.use_continuous_actions(full_observations=True)
+    cfg.scene.num_envs = E
+    cfg.seed = seed
+    env = env_cls(cfg, device=gpu_device)
+    return env, cfg
+
+
+@pytest.mark.parametrize("name,env_name,variant,E,full_obs", [
+    # C5: OC2 XOR cyclamen, continuous wheels, 24-D full observations, 4096 envs per GPU
+    ("C5 XOR oc2 continuous", "XorAggregationEnv", "cyclamen", 4096, True),
+    # C3: Foraging cyclamen, discrete module ids, 4-D observations, 8192 envs
+    ("C3 Foraging cyclamen", "ForagingEnv", "cyclamen", 8192, False),
+])
+def test_production_kernel_config_workloads(name, env_name, variant, E, full_obs, gpu_device):
+    """The per-GPU workloads of BASELINE configs C3 and C5 at their full size, built
+    from the cfg classes the configs use, element by element against the oracle
+    (the same staggered time-outs as test_production_kernel_vs_oracle)."""
+    from SwarmACB_isaac import env as envs
+
+    seed = 30300 + E
+    env, cfg = _config_engine(getattr(envs, env_name), variant, E, seed, gpu_device, full_obs)
+    eng = env.engine
+    assert eng.obs_dim == (24 if full_obs else 4) and eng.discrete == (not full_obs)
+    assert eng.max_episode_length == 1800
+    eng.reset()
+    _stagger_timeouts(eng, [(np.arange(3, 13), 3), (np.arange(E // 2, E // 2 + 7), 17), ([E - 1], 31),
+                            (np.arange(100, 140), 44)])
+    rng = np.random.default_rng(E + 1)
+    acts = [rng.integers(0, 6, (E, 20)) if eng.discrete else (np.clip(rng.normal(size=(E, 20, 2)), -3, 3) / 3)
+            for _ in range(10)]
+    mission = env.mission
+    run_cfg = (mission, "isaac", E, 20, eng.obs_dim, eng.discrete, eng.max_episode_length)
+    stats, n_to = _teacher_forced(eng, run_cfg, lambda k: acts[k // 5], 50, seed, tag=name)
+    env.close()
     assert n_to >= 10 + 7 + 1 + 40
     _report(name, stats)
 

@@ -125,6 +125,55 @@ def test_option_playback_policy_call_and_return_on_cpu(tmp_path):
     assert w.shape == (3, 4, 2) and float(w.abs().max()) <= 1.0
 
 
+class _FinishingEnv:
+    """CPU stand-in of the env surface evaluate() uses: env 1 finishes at its 3rd step,
+    every env at its 8th."""
+
+    def __init__(self, E, N, D):
+        self.num_envs, self.device, self.D = E, torch.device("cpu"), D
+        self.possible_agents = [f"epuck_{i}" for i in range(N)]
+        self.t = 0
+
+    def reset(self):
+        return {a: torch.randn(self.num_envs, self.D) for a in self.possible_agents}, {}
+
+    def step(self, action_dict):
+        self.t += 1
+        done = torch.zeros(self.num_envs, dtype=torch.bool)
+        if self.t == 3:
+            done[1] = True
+        if self.t == 8:
+            done[:] = True
+        agents = self.possible_agents
+        obs = {a: torch.randn(self.num_envs, self.D) for a in agents}
+        return (obs, {a: torch.ones(self.num_envs) for a in agents},
+                {a: torch.zeros_like(done) for a in agents}, {a: done for a in agents}, {})
+
+
+@pytest.mark.parametrize("kind,expect", [("oc", 0), ("oc2", -1)])
+def test_finished_env_option_after_reset_follows_reference(tmp_path, kind, expect):
+    """play.py:640-641 / 689 / 703: the fixed-option action dict aliases current_options, so
+    the finished env's option is -1 then overwritten by 0 (no forced reselection next
+    decision); the learned-option actions are wheel samples, so its option stays -1."""
+    paths, _, _ = _option_checkpoints(tmp_path)
+    D = 4 if kind == "oc" else 24
+    net, info = CK.actor_from_checkpoint(str(paths[kind]), D)
+    pol = CK.PlaybackPolicy(net, 3, 4, "cpu", deterministic=True, option_epsilon=info["option_epsilon"],
+                            action_transform=info["action_transform"])
+    seen = []
+    real_act = pol.act
+
+    def act(obs):
+        seen.append(pol.current_options.clone())
+        return real_act(obs)
+
+    pol.act = act
+    rewards = CK.evaluate(_FinishingEnv(3, 4, D), pol, num_episodes=2, decision_period=5, deterministic=True)
+    assert len(seen) >= 2 and rewards[0] == 3.0
+    assert bool((seen[1][1] == expect).all())
+    assert bool((seen[1][0] >= 0).all())
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,task", [("oc", "SwarmACB-DirectionalGate-v0"), ("oc2", "SwarmACB-XOR-v0")])
 def test_play_option_checkpoints_on_gpu(tmp_path, gpu_device, kind, task):
