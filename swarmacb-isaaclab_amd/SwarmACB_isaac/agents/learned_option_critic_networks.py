@@ -46,9 +46,9 @@ class SquashedNormal:
 
     _EPS = 1e-6
 
-    def __init__(self, loc: torch.Tensor, scale: torch.Tensor):
+    def __init__(self, loc: torch.Tensor, scale: torch.Tensor, validate_args: bool | None = None):
         self.loc, self.scale = loc, scale
-        self.base_dist = Normal(loc, scale, validate_args=False)
+        self.base_dist = Normal(loc, scale, validate_args=validate_args)
 
     @property
     def mean(self) -> torch.Tensor:

@@ -98,6 +98,27 @@
 #define SWARM_CR_SQRT 1
 #endif
 
+// 1: the per-lane candidate loops (contact pairs, proximity discs, range-and-bearing
+// terms) are software-pipelined: the LDS read of the next candidate's position is
+// issued before the current candidate's arithmetic, so its latency overlaps the
+// sqrt / rcp chain instead of starting every trip. Same terms in the same order.
+#ifndef SWARM_PIPE_LOOPS
+#define SWARM_PIPE_LOOPS 0
+#endif
+
+// Verlet-style reuse of the contact candidates across the push iterations of one
+// solver call: the pairs closer than min_dist + margin are listed once and kept
+// until some robot of the arena has moved more than margin / 2 since (a pair's
+// distance then changed by less than the margin, so no contact is missed). The
+// exact sqrt test of every listed pair stays, so results are unchanged.
+// 0: candidates rebuilt every iteration.
+#ifndef SWARM_VERLET
+#define SWARM_VERLET 0
+#endif
+#ifndef SWARM_VERLET_MARGIN
+#define SWARM_VERLET_MARGIN 0.004f
+#endif
+
 // Diagnostic build only (tools/wave_timing.py): each wave of the production step
 // kernel records its start / end shader clock, hardware slot and work counters.
 #ifndef SWARM_WAVE_TIMING
@@ -332,6 +353,41 @@ __device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, 
     return m;
 }
 
+// f(j, p_j) for every candidate j of this part's chunk (bits of `cand`), in
+// increasing j. SWARM_PIPE_LOOPS: the next candidate's tile entry is read before
+// f runs on the current one.
+template <class F>
+__device__ __forceinline__ void for_each_cand(const Lane& L, const float2* xy, uint32_t cand, F f) {
+#if SWARM_PIPE_LOOPS
+    if (!cand) return;
+    int j = L.j0 + __builtin_ctz(cand);
+    cand &= cand - 1u;
+    float2 p = xy[L.ab + j];
+    for (;;) {
+        const int jn = cand ? L.j0 + __builtin_ctz(cand) : j;
+        const float2 pn = xy[L.ab + jn];
+        f(j, p);
+        if (!cand) break;
+        cand &= cand - 1u;
+        j = jn;
+        p = pn;
+    }
+#else
+    while (cand) {
+        const int j = L.j0 + __builtin_ctz(cand);
+        cand &= cand - 1u;
+        f(j, xy[L.ab + j]);
+    }
+#endif
+}
+
+// Candidate list of the contact solver kept across push iterations (SWARM_VERLET).
+struct PairList {
+    uint32_t cand;
+    float bx, by;       // this robot's position when the list was built
+    bool built;         // wave-uniform
+};
+
 // ---------------------------------------------------------------------------
 //  Collisions
 // ---------------------------------------------------------------------------
@@ -388,7 +444,8 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 // Returns false only when it is known (wave-uniformly) that no pair term
 // contributed, i.e. the push was the identity map on every lane.
 template <int LY, int C>
-__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
+__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y,
+                                            PairList* vl = nullptr) {
     if (SWARM_ABLATE & 4) return false;
     SWARM_WT(L.wt_push++);
     if (L.p == 0) S.xy[L.r] = make_float2(x, y);
@@ -428,16 +485,31 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         }
     } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
-        uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
-            return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
-        });
-        while (cand) {
-            SWARM_WT(L.wt_pair++);
-            const int j = L.j0 + __builtin_ctz(cand);
-            cand &= cand - 1u;
-            const float2 p = S.xy[L.ab + j];
-            pair_term(j, x - p.x, y - p.y);
+        uint32_t cand;
+        if (SWARM_VERLET && vl) {
+            // rebuild unless every robot of the arena moved less than margin / 2 since
+            // the last build (then |d_ij| changed by less than the margin)
+            const float mx = x - vl->bx, my = y - vl->by;
+            constexpr float h = 0.5f * SWARM_VERLET_MARGIN;
+            if (!vl->built || __any(mx * mx + my * my >= h * h)) {
+                const float vd = g.min_dist + SWARM_VERLET_MARGIN, vd2 = vd * vd * 1.0001f;
+                vl->cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
+                    return dx * dx + dy * dy + 1e-8f < vd2;
+                });
+                vl->bx = x;
+                vl->by = y;
+                vl->built = true;
+            }
+            cand = vl->cand;
+        } else {
+            cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
+                return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
+            });
         }
+        for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
+            SWARM_WT(L.wt_pair++);
+            pair_term(j, x - p.x, y - p.y);
+        });
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -619,12 +691,13 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     gate_walls<MISSION, ISAAC>(g, x, y);
     constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
     bool fixed = false;                                   // wave-uniform
+    PairList vl{0u, 0.0f, 0.0f, false};
 #pragma unroll
     for (int it = 0; it <= K; ++it) {
         if (fixed && it < K) continue;
         const float bx = x, by = y;
         bool pushed = false;
-        if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
+        if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y, &vl);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
@@ -797,14 +870,12 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             if (j < L.j1 && j != L.i && dx * dx + dy * dy <= 0.0200f) disc(dx, dy);
         }
     } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
-        uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
-        while (cand) {
+        const uint32_t cand = chunk_mask<C>(L, S.xy, x, y,
+                                            [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
+        for_each_cand(L, S.xy, cand, [&](int, float2 p) {
             SWARM_WT(L.wt_disc++);
-            const int j = L.j0 + __builtin_ctz(cand);
-            cand &= cand - 1u;
-            const float2 p = S.xy[L.ab + j];
             disc(p.x - x, p.y - y);
-        }
+        });
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -970,13 +1041,10 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
                 kept |= (((cand >> jj) & 1u) && uu >= g.rab_loss) ? (1u << jj) : 0u;
             }
         }
-        while (kept) {
+        for_each_cand(L, xy, kept, [&](int j, float2 q) {
             SWARM_WT(L.wt_rab++);
-            const int j = L.j0 + __builtin_ctz(kept);
-            kept &= kept - 1u;
-            const float2 q = xy[L.ab + j];
             term(j, q.x - x, q.y - y);
-        }
+        });
     } else {
         unsigned long long cand = 0;
 #pragma unroll

@@ -220,7 +220,7 @@ def run_case(LOT, name, *, E, N, R, dp, cfg_kw, seed, do_update):
     print(f"wrote {path}")
 
 
-def main():
+def main(only=()):
     LOT = import_oc2()
     common = dict(lr_schedule="linear", eps_schedule="linear", beta_schedule="linear", total_timesteps=4000,
                   reward_strength=0.8, num_epochs=2, num_options=6, matmul_precision="highest",
@@ -228,21 +228,38 @@ def main():
                   termination_prior_coef=0.02, termination_prior_final_coef=0.01, option_balance_coef=0.01,
                   termination_entropy_coef=0.001, option_entropy_coef=0.001, termination_penalty=0.01,
                   adaptive_actor_lr=True, initial_log_std=-0.5)
-    run_case(LOT, "oc2_update", E=6, N=4, R=6, dp=5, seed=7, do_update=True,
-             cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=3,
-                         option_hidden_dim=16, option_num_layers=2, option_memory_size=8, critic_hidden_dim=16,
-                         critic_num_layers=1, critic_num_heads=2, mini_batch_size=12, target_kl=0.05))
-    # tiny KL budget: the actor stops after the first minibatch, the critics continue
-    run_case(LOT, "oc2_update_kl", E=4, N=4, R=4, dp=5, seed=9, do_update=True,
-             cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=2,
-                         option_hidden_dim=16, option_num_layers=1, option_memory_size=8, critic_hidden_dim=16,
-                         critic_num_layers=1, critic_num_heads=2, mini_batch_size=8, target_kl=1e-6,
-                         num_epochs=1))
-    run_case(LOT, "oc2_collect_h128", E=6, N=4, R=6, dp=5, seed=8, do_update=False,
-             cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=8,
-                         option_hidden_dim=64, option_num_layers=2, option_memory_size=16, critic_hidden_dim=128,
-                         critic_num_layers=1, critic_num_heads=4))
+    cases = {
+        "oc2_update": lambda: run_case(
+            LOT, "oc2_update", E=6, N=4, R=6, dp=5, seed=7, do_update=True,
+            cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=3,
+                        option_hidden_dim=16, option_num_layers=2, option_memory_size=8, critic_hidden_dim=16,
+                        critic_num_layers=1, critic_num_heads=2, mini_batch_size=12, target_kl=0.05)),
+        # tiny KL budget: the actor stops after the first minibatch, the critics continue
+        "oc2_update_kl": lambda: run_case(
+            LOT, "oc2_update_kl", E=4, N=4, R=4, dp=5, seed=9, do_update=True,
+            cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=2,
+                        option_hidden_dim=16, option_num_layers=1, option_memory_size=8, critic_hidden_dim=16,
+                        critic_num_layers=1, critic_num_heads=2, mini_batch_size=8, target_kl=1e-6,
+                        num_epochs=1)),
+        "oc2_collect_h128": lambda: run_case(
+            LOT, "oc2_collect_h128", E=6, N=4, R=6, dp=5, seed=8, do_update=False,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=8,
+                        option_hidden_dim=64, option_num_layers=2, option_memory_size=16, critic_hidden_dim=128,
+                        critic_num_layers=1, critic_num_heads=4)),
+        # configs/OC2_XOR_cyclamen.yaml network sizes (hidden / option hidden 128, memories 128, critics
+        # 128 x 4 heads, target_kl 0.01) and 20 e-pucks: 4 envs x 4 decisions, ONE minibatch of 160
+        # sequences (546 k parameters: one actor and one critic step keep the file at a few MB)
+        "oc2_update_h128": lambda: run_case(
+            LOT, "oc2_update_h128", E=4, N=20, R=4, dp=5, seed=13, do_update=True,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
+                        option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=320,
+                        target_kl=0.01, num_epochs=1)),
+    }
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -192,17 +192,30 @@ def run_case(OCT, name, *, E, N, D, R, dp, cfg_kw, seed, do_update):
     print(f"wrote {path}: {len(log.cat)} option samples, {len(log.bern)} termination samples")
 
 
-def main():
+def main(only=()):
     OCT = import_oc()
     common = dict(lr_schedule="linear", eps_schedule="linear", beta_schedule="linear", total_timesteps=2000,
                   reward_strength=0.8, num_epochs=2, num_options=N_OPTIONS)
-    run_case(OCT, "oc_update", E=6, N=4, D=4, R=6, dp=5, seed=5, do_update=True,
-             cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=3,
-                         critic_hidden_dim=16, critic_num_layers=1, critic_num_heads=2, mini_batch_size=12))
-    run_case(OCT, "oc_collect_h128", E=6, N=4, D=4, R=6, dp=5, seed=6, do_update=False,
-             cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=8,
-                         critic_hidden_dim=128, critic_num_layers=2, critic_num_heads=4))
+    cases = {
+        "oc_update": lambda: run_case(
+            OCT, "oc_update", E=6, N=4, D=4, R=6, dp=5, seed=5, do_update=True,
+            cfg_kw=dict(common, hidden_dim=16, num_layers=1, memory_size=16, sequence_length=3,
+                        critic_hidden_dim=16, critic_num_layers=1, critic_num_heads=2, mini_batch_size=12)),
+        "oc_collect_h128": lambda: run_case(
+            OCT, "oc_collect_h128", E=6, N=4, D=4, R=6, dp=5, seed=6, do_update=False,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=8,
+                        critic_hidden_dim=128, critic_num_layers=2, critic_num_heads=4)),
+        # configs/OC_DirGate_cyclamen.yaml network sizes, 20 e-pucks: 4 envs x 4 decisions, 2 minibatches
+        "oc_update_h128": lambda: run_case(
+            OCT, "oc_update_h128", E=4, N=20, D=4, R=4, dp=5, seed=12, do_update=True,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=160,
+                        num_epochs=1)),
+    }
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -19,7 +19,7 @@ Cases: feedforward continuous (dandelion-like, get_batches) and recurrent
 discrete (cyclamen-like, get_sequence_batches with critic memories), both with
 linear lr / epsilon / beta schedules.
 
-Usage: python tests/golden/trainer/make_trainer_golden.py
+Usage: python tests/golden/trainer/make_trainer_golden.py [case ...]   (default: every case)
 """
 
 from __future__ import annotations
@@ -124,16 +124,29 @@ def run_case(PT, name, *, discrete, recurrent, E, N, D, R, dp, cfg_kw, seed):
     print(f"wrote {path}: {len(grads)} optimizer steps, {len(perms)} permutations, metrics {metrics}")
 
 
-def main():
+def main(only=()):
     PT = import_trainer()
     common = dict(hidden_dim=16, num_layers=2, critic_hidden_dim=16, critic_num_layers=1, critic_num_heads=2,
                   lr_schedule="linear", eps_schedule="linear", beta_schedule="linear", total_timesteps=2000,
                   reward_strength=1.0, num_epochs=2)
-    run_case(PT, "poca_update_ff", discrete=False, recurrent=False, E=6, N=4, D=24, R=5, dp=5,
-             cfg_kw=dict(common, mini_batch_size=32), seed=3)
-    run_case(PT, "poca_update_rnn", discrete=True, recurrent=True, E=6, N=4, D=4, R=5, dp=5,
-             cfg_kw=dict(common, mini_batch_size=8, memory_size=16, sequence_length=2, num_layers=1), seed=4)
+    cases = {
+        "poca_update_ff": lambda: run_case(PT, "poca_update_ff", discrete=False, recurrent=False, E=6, N=4, D=24, R=5,
+                                           dp=5, cfg_kw=dict(common, mini_batch_size=32), seed=3),
+        "poca_update_rnn": lambda: run_case(PT, "poca_update_rnn", discrete=True, recurrent=True, E=6, N=4, D=4, R=5,
+                                            dp=5, cfg_kw=dict(common, mini_batch_size=8, memory_size=16,
+                                                              sequence_length=2, num_layers=1), seed=4),
+        # the network sizes of configs/Foraging_cyclamen.yaml (hidden 128, memory 128, 1 layer, critic
+        # 128 x 4 heads) and 20 e-pucks; 4 envs x 4 decisions, sequences of 2 -> 160 chunks, 2 minibatches
+        "poca_update_rnn_h128": lambda: run_case(
+            PT, "poca_update_rnn_h128", discrete=True, recurrent=True, E=4, N=20, D=4, R=4, dp=5,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=160,
+                        num_epochs=1), seed=11),
+    }
+    for name, fn in cases.items():
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))

@@ -39,7 +39,12 @@ OC2_CASES = {
                              option_num_layers=2, option_memory_size=16, critic_hidden_dim=128, critic_num_layers=1,
                              critic_num_heads=4),
 }
-UPDATE_CASES = ("oc2_update", "oc2_update_kl")
+# configs/OC2_XOR_cyclamen.yaml network sizes, 20 e-pucks
+OC2_CASES["oc2_update_h128"] = dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
+                                    option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
+                                    critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4,
+                                    mini_batch_size=320, target_kl=0.01, num_epochs=1)
+UPDATE_CASES = ("oc2_update", "oc2_update_kl", "oc2_update_h128")
 MODULES = ("actor", "team_critic", "action_critic", "option_critic")
 
 
@@ -193,9 +198,13 @@ def check_metrics(metrics, fx):
         if k in exact:
             assert g == r or abs(g - r) <= 1e-12 * max(1.0, abs(r)), (k, g, r)
         elif "kl" in k or k.endswith("logp_error"):
-            # exp(x) - 1 - x at |x| ~ 1e-3 cancels in fp32: ~1 % per element (the early-stop
-            # decisions themselves are compared exactly through kl_early_stop / actor_updates)
-            assert abs(g - r) <= 2e-2 * abs(r) + 2e-7, (k, g, r)
+            # KL terms are means of exp(d) - 1 - d with d = a log-ratio of ~1e-3: exp(d) ~ 1 is
+            # rounded to within eps32 / 2 = 6e-8 ABSOLUTE on either side (SLEEF in the reference,
+            # ocml here), on terms of ~5e-7, so a mean differs by at most ~2 eps32 absolute, not
+            # by a relative amount; the logp-error diagnostics are means of such rounding
+            # residues themselves. Bar: 1e-4 relative + 2 eps32 absolute (the early-stop
+            # decisions are compared exactly through kl_early_stop / actor_updates).
+            assert abs(g - r) <= 1e-4 * abs(r) + 2.0 * 2.0 ** -23, (k, g, r)
         else:
             assert abs(g - r) <= 1e-4 * abs(r) + 1e-5 * max(1.0, abs(r)), (k, g, r)
     for k in ("option_usage", "option_betas", "option_switch_rates", "option_termination_counts", "option_stds"):

@@ -32,7 +32,11 @@ OC_CASES = {
                       critic_num_layers=1, critic_num_heads=2, mini_batch_size=12),
     "oc_collect_h128": dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=8, critic_hidden_dim=128,
                             critic_num_layers=2, critic_num_heads=4),
+    # configs/OC_DirGate_cyclamen.yaml network sizes, 20 e-pucks
+    "oc_update_h128": dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2, critic_hidden_dim=128,
+                           critic_num_layers=1, critic_num_heads=4, mini_batch_size=160, num_epochs=1),
 }
+UPDATE_CASES = ("oc_update", "oc_update_h128")
 OC_LOSS_NAMES = ("policy", "value", "joint_option_value", "baseline", "termination", "option_entropy",
                  "termination_entropy", "mean_beta", "mean_option_advantage")
 
@@ -104,7 +108,7 @@ def make_oc_trainer(name, device, env=None):
 
     fx = load(name)
     E, N, D, R, dp = (int(x) for x in fx["meta"])
-    cfg = FixedOptionCriticConfig(horizon=R, log_dir="/tmp/_oc_test_runs", **OC_COMMON, **OC_CASES[name])
+    cfg = FixedOptionCriticConfig(horizon=R, log_dir="/tmp/_oc_test_runs", **dict(OC_COMMON, **OC_CASES[name]))
     env = env if env is not None else ReplayEnv(fx, device)
     tr = FixedOptionCriticTrainer(env, cfg, writer=NullWriter())
     named = dict([("manager." + k, p) for k, p in tr.manager.named_parameters()] +

@@ -65,8 +65,9 @@ def test_oc_collect_matches_reference(name, gpu_device):
     print(f"[oc collect] {name}: worst relative error {max(worst.values()):.3g} ({max(worst, key=worst.get)})")
 
 
-def test_oc_update_on_gpu_matches_reference(gpu_device):
-    tf, metrics, fx = OF.run_teacher_forced_oc("oc_update", gpu_device)
+@pytest.mark.parametrize("name", OF.UPDATE_CASES)
+def test_oc_update_on_gpu_matches_reference(name, gpu_device):
+    tf, metrics, fx = OF.run_teacher_forced_oc(name, gpu_device)
     ref = dict(zip([str(k) for k in fx["metrics_keys"]], fx["metrics_values"]))
     for k in ("lr", "eps", "beta"):
         assert metrics[k] == pytest.approx(ref[k], rel=1e-12)
@@ -78,8 +79,9 @@ def test_oc_update_on_gpu_matches_reference(gpu_device):
           f"max param err {tf.max_param_err:.3g}")
 
 
-def test_oc_update_on_gpu_with_host_batches(gpu_device):
-    tf, _, _ = OF.run_teacher_forced_oc("oc_update", gpu_device, batches="oracle")
+@pytest.mark.parametrize("name", OF.UPDATE_CASES)
+def test_oc_update_on_gpu_with_host_batches(name, gpu_device):
+    tf, _, _ = OF.run_teacher_forced_oc(name, gpu_device, batches="oracle")
     assert tf.steps > 0
 
 

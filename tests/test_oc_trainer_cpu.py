@@ -13,10 +13,11 @@ import torch
 import oc_fixtures as OF
 
 
-def test_oc_update_teacher_forced_cpu():
-    tf, _, fx = OF.run_teacher_forced_oc("oc_update", "cpu", batches="oracle")
+@pytest.mark.parametrize("name", OF.UPDATE_CASES)
+def test_oc_update_teacher_forced_cpu(name):
+    tf, _, fx = OF.run_teacher_forced_oc(name, "cpu", batches="oracle")
     assert tf.steps == int(fx["n_steps"]) > 0
-    print(f"oc_update: {tf.steps} steps, max grad err {tf.max_grad_err:.3g}, max param err {tf.max_param_err:.3g}")
+    print(f"{name}: {tf.steps} steps, max grad err {tf.max_grad_err:.3g}, max param err {tf.max_param_err:.3g}")
 
 
 def test_manager_state_dict_matches_reference_names():

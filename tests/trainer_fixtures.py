@@ -23,6 +23,10 @@ CASES = {
     "poca_update_ff": (False, False, 6, 4, 24, dict(mini_batch_size=32, num_layers=2, seed=3)),
     "poca_update_rnn": (True, True, 6, 4, 4, dict(mini_batch_size=8, memory_size=16, sequence_length=2,
                                                   num_layers=1, seed=4)),
+    # configs/Foraging_cyclamen.yaml network sizes (hidden 128, memory 128, critic 128 x 4 heads), 20 e-pucks
+    "poca_update_rnn_h128": (True, True, 4, 20, 4, dict(mini_batch_size=160, memory_size=128, sequence_length=2,
+                                                        num_layers=1, seed=11, hidden_dim=128, critic_hidden_dim=128,
+                                                        critic_num_heads=4, num_epochs=1, horizon=4)),
 }
 COMMON = dict(hidden_dim=16, critic_hidden_dim=16, critic_num_layers=1, critic_num_heads=2, lr_schedule="linear",
               eps_schedule="linear", beta_schedule="linear", total_timesteps=2000, reward_strength=1.0, num_epochs=2,
@@ -61,7 +65,7 @@ def make_trainer(name, device, writer=None):
 
     discrete, recurrent, E, N, D, kw = CASES[name]
     fx = load(name)
-    cfg = POCAConfig(recurrent=recurrent, log_dir="/tmp/_poca_test_runs", **COMMON, **kw)
+    cfg = POCAConfig(recurrent=recurrent, log_dir="/tmp/_poca_test_runs", **dict(COMMON, **kw))
     tr = POCATrainer(StubEnv(E, N, D, discrete, device), cfg, writer=writer or NullWriter())
     named = dict([("actor." + k, p) for k, p in tr.actor.named_parameters()] +
                  [("critic." + k, p) for k, p in tr.critic.named_parameters()])
