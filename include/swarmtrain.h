@@ -56,6 +56,19 @@ int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float
                                 const float* dh_n, const float* dc_n, float* dxg, float* dh0, float* dc0,
                                 void* stream);
 
+/* Training-time attention core of ResidualSelfAttention (reference agents/poca_networks.py:417-491,
+ * replaces the autograd bmm / softmax / bmm path of every PPO optimizer step): per entity set s
+ * (S sets of N <= 32 entities) and head h (H heads of d = D / H in {32, 64, 128} columns),
+ *     att[s, :, h] = softmax_j( (q k^T) / sqrt(D) + key_mask[s] * (-1e6) ) v
+ * with q | k | v the column blocks [0, D), [D, 2D), [2D, 3D) of qkv: [S*N][3D] (the fused input
+ * projection, row s*N + n = entity n of set s) and att: [S*N][D]. key_mask: [S][N] f32 (1 = masked) or
+ * NULL. The contractions run on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums in another order
+ * than torch's). The backward recomputes the probabilities and writes d_qkv: [S*N][3D] (every element). */
+int32_t swarm_rsa_attn_forward(int64_t S, int32_t N, int32_t H, int32_t D, const float* qkv, const float* key_mask,
+                               float* att, void* stream);
+int32_t swarm_rsa_attn_backward(int64_t S, int32_t N, int32_t H, int32_t D, const float* qkv, const float* key_mask,
+                                const float* d_att, float* d_qkv, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -69,6 +69,7 @@ def _mlagents_lstm(input_size: int, memory_size: int, forget_bias: float = 1.0) 
 
 
 FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of the reference path)
+FUSED_ATTENTION = True   # False: ResidualSelfAttention's core runs torch's bmm / softmax path
 
 
 def _plain_lstm(lstm: nn.LSTM) -> bool:
@@ -121,6 +122,37 @@ class _LSTMSequence(torch.autograd.Function):
             h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
             dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
         return dxg, dw, dh0, dc0, None
+
+
+class _AttnCore(torch.autograd.Function):
+    """softmax((q k^T) / sqrt(D) + key_mask * NEG_INF) v per entity set and head on
+    swarm_rsa_attn_forward / _backward (include/swarmtrain.h, v_mfma_f32_16x16x4_f32):
+    qkv (S*N, 3D) is the fused q | k | v projection, key_mask (S, N) f32 or None;
+    returns att (S*N, D). The backward recomputes the probabilities."""
+
+    @staticmethod
+    def forward(ctx, qkv, key_mask, S: int, N: int, H: int):
+        D = qkv.shape[1] // 3
+        att = torch.empty(S * N, D, dtype=qkv.dtype, device=qkv.device)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+        _native.check(lib.swarm_rsa_attn_forward(S, N, H, D, _ptr(qkv), _ptr(key_mask), _ptr(att), stream),
+                      "swarm_rsa_attn_forward")
+        ctx.save_for_backward(qkv, key_mask)
+        ctx.dims = (S, N, H, D)
+        return att
+
+    @staticmethod
+    def backward(ctx, d_att):
+        qkv, key_mask = ctx.saved_tensors
+        S, N, H, D = ctx.dims
+        d_qkv = torch.empty_like(qkv)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
+        _native.check(lib.swarm_rsa_attn_backward(S, N, H, D, _ptr(qkv), _ptr(key_mask), _ptr(d_att.contiguous()),
+                                                  _ptr(d_qkv), stream),
+                      "swarm_rsa_attn_backward")
+        return d_qkv, None, None, None, None
 
 
 def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
@@ -325,15 +357,29 @@ class ResidualSelfAttention(nn.Module):
         self.embedding_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
         self.residual_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
 
+    def _native_core(self, inp: torch.Tensor) -> bool:
+        B, N, D = inp.shape
+        return (FUSED_ATTENTION and inp.is_cuda and inp.dtype == torch.float32 and B > 0
+                and 1 <= N <= _native.ATTN_MAX_ENTITIES and self.head_dim in _native.ATTN_HEAD_DIMS)
+
     def forward(self, inp: torch.Tensor, key_mask: torch.Tensor | None = None) -> torch.Tensor:
         B, N, D = inp.shape
         H, d = self.num_heads, self.head_dim
         x = self.embedding_norm(inp)
-        heads = [f(x).view(B, N, H, d).transpose(1, 2) for f in (self.fc_q, self.fc_k, self.fc_v)]
-        logits = (heads[0] @ heads[1].transpose(-2, -1)) / math.sqrt(D)
-        if key_mask is not None:
-            logits = logits + key_mask.view(B, 1, 1, N) * self.NEG_INF
-        att = (logits.softmax(dim=-1) @ heads[2]).transpose(1, 2).contiguous().view(B, N, D)
+        if self._native_core(inp):
+            # the three projections as one GEMM (q | k | v column blocks), then the attention
+            # core of every set and head in one MFMA kernel each way (_AttnCore)
+            w = torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight])
+            b = torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias])
+            qkv = torch.nn.functional.linear(x.reshape(B * N, D), w, b).contiguous()
+            km = key_mask.reshape(B, N).to(torch.float32).contiguous() if key_mask is not None else None
+            att = _AttnCore.apply(qkv, km, B, N, H).view(B, N, D)
+        else:
+            heads = [f(x).view(B, N, H, d).transpose(1, 2) for f in (self.fc_q, self.fc_k, self.fc_v)]
+            logits = (heads[0] @ heads[1].transpose(-2, -1)) / math.sqrt(D)
+            if key_mask is not None:
+                logits = logits + key_mask.view(B, 1, 1, N) * self.NEG_INF
+            att = (logits.softmax(dim=-1) @ heads[2]).transpose(1, 2).contiguous().view(B, N, D)
         out = self.residual_norm(self.fc_out(att) + x)
         if key_mask is None:
             return out.mean(dim=1)

@@ -24,70 +24,105 @@ constexpr int NT = 256;
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U, const float* __restrict__ xg,
+// Steps per prefetch group. A loop-carried register copy of a global load makes the
+// compiler wait for it (and, vmcnt being in order, for every store issued before
+// it), so loading one step ahead still paid a global round trip per step; here the
+// inputs of the next PF steps are loaded (unconditionally, clamped addresses: no
+// divergent branch around a load, which would make the waits conservative) while
+// the current PF unrolled steps run, and the round trip is paid once per group.
+// The unit count is a template parameter (UC, 0 = runtime) so the inner products
+// have no runtime bounds branches either.
+constexpr int PF = 8;
+constexpr int PB = 4;
+
+template <int UC, bool KEEP>
+__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
                                                           const float* __restrict__ w_hh,
                                                           const float* __restrict__ h0,
                                                           const float* __restrict__ c0,
                                                           const float* __restrict__ keep, float* __restrict__ h_out,
                                                           float* __restrict__ c_out, float* __restrict__ act) {
+    constexpr int KU = UC > 0 ? UC : MAXU;              // register extent of a gate row
+    const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float hs[MAXU];
     __shared__ float gs[4 * MAXU];
     const int64_t b = blockIdx.x;
     const int j = threadIdx.x;
     const int G = 4 * U;
-    float w[MAXU];
+    const bool row_j = (UC == MAXU) || j < G;           // thread j owns gate pre-activation j
+    const int jc = row_j ? j : G - 1;                    // clamped: loads never leave the row
+    float w[KU];
 #pragma unroll
-    for (int k = 0; k < MAXU; ++k) w[k] = (j < G && k < U) ? w_hh[j * U + k] : 0.0f;
+    for (int k = 0; k < KU; ++k) w[k] = (row_j && k < U) ? w_hh[jc * U + k] : 0.0f;
     float c = 0.0f;
     if (j < MAXU) hs[j] = j < U ? h0[b * U + j] : 0.0f;   // padded to a multiple of 4 for float4 reads
     if (j < U) c = c0[b * U + j];
-    const int kind = j / (U > 0 ? U : 1);                // 0 i, 1 f, 2 g, 3 o
-    // the step's global inputs are loaded one step ahead, off the recurrence's critical path
-    float x_next = j < G ? xg[b * T * G + j] : 0.0f;
-    float k_next = (keep && j < U) ? keep[b * T] : 1.0f;
-    __syncthreads();
-    for (int t = 0; t < T; ++t) {
-        const int64_t row = b * T + t;
-        const float x = x_next, kk = (t + 1 < T) ? k_next : 1.0f;
-        if (t + 1 < T) {
-            if (j < G) x_next = xg[(row + 1) * G + j];
-            if (keep && j < U) k_next = keep[row + 1];
-        }
-        if (j < G) {
-            // four independent accumulation chains (16 deep at 64 units)
-            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    const int kind = j / U;                              // 0 i, 1 f, 2 g, 3 o
+    // inputs of step t: the gate pre-activation x W_ih^T + b and the keep applied to
+    // the state carried into t + 1 (1 after the last step)
+    const float* xb = xg + b * T * G + jc;
+    auto load_group = [&](int t0, float* xr, float* kr) {
 #pragma unroll
-            for (int k = 0; k < MAXU; k += 8)
-                if (k < U) {
-                    const float4 h4 = *reinterpret_cast<const float4*>(&hs[k]);
-                    a0 += w[k] * h4.x + w[k + 2] * h4.z;
-                    a1 += w[k + 1] * h4.y + w[k + 3] * h4.w;
-                    if (k + 4 < U) {
-                        const float4 g4 = *reinterpret_cast<const float4*>(&hs[k + 4]);
-                        a2 += w[k + 4] * g4.x + w[k + 6] * g4.z;
-                        a3 += w[k + 5] * g4.y + w[k + 7] * g4.w;
+        for (int p = 0; p < PF; ++p) {
+            const int t = min(t0 + p, T - 1);
+            xr[p] = xb[(int64_t)t * G];
+            if constexpr (KEEP) kr[p] = keep[b * T + t];
+        }
+    };
+    float xr[PF], kr[PF] = {};
+    load_group(0, xr, kr);
+    __syncthreads();
+    for (int t0 = 0; t0 < T; t0 += PF) {
+        float xn[PF], kn[PF] = {};
+        load_group(t0 + PF, xn, kn);
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            const int t = t0 + p;
+            if (t >= T) break;
+            const int64_t row = b * T + t;
+            if (row_j) {
+                // four independent accumulation chains (16 deep at 64 units)
+                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+#pragma unroll
+                for (int k = 0; k < KU; k += 8)
+                    if (UC > 0 || k < U) {
+                        const float4 h4 = *reinterpret_cast<const float4*>(&hs[k]);
+                        a0 += w[k] * h4.x + w[k + 2] * h4.z;
+                        a1 += w[k + 1] * h4.y + w[k + 3] * h4.w;
+                        if (k + 4 < KU && (UC > 0 || k + 4 < U)) {
+                            const float4 g4 = *reinterpret_cast<const float4*>(&hs[k + 4]);
+                            a2 += w[k + 4] * g4.x + w[k + 6] * g4.z;
+                            a3 += w[k + 5] * g4.y + w[k + 7] * g4.w;
+                        }
                     }
-                }
-            const float a = ((a0 + a1) + (a2 + a3)) + x;
-            const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
-            gs[j] = v;
-            act[row * G + j] = v;
+                const float a = ((a0 + a1) + (a2 + a3)) + xr[p];
+                const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
+                gs[j] = v;
+                act[row * G + j] = v;
+            }
+            __syncthreads();
+            if (j < U) {
+                c = gs[U + j] * c + gs[j] * gs[2 * U + j];
+                const float h = gs[3 * U + j] * tanhf(c);
+                h_out[row * U + j] = h;
+                c_out[row * U + j] = c;
+                // the state carried into step t + 1 is masked where the episode ended at t
+                const float kk = (KEEP && t + 1 < T) ? kr[p] : 1.0f;
+                hs[j] = h * kk;
+                c *= kk;
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (j < U) {
-            c = gs[U + j] * c + gs[j] * gs[2 * U + j];
-            const float h = gs[3 * U + j] * tanhf(c);
-            h_out[row * U + j] = h;
-            c_out[row * U + j] = c;
-            // the state carried into step t + 1 is masked where the episode ended at t
-            hs[j] = h * kk;
-            c *= kk;
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            xr[p] = xn[p];
+            kr[p] = kn[p];
         }
-        __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const float* __restrict__ w_hh,
+template <int UC, bool KEEP>
+__global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const float* __restrict__ w_hh,
                                                           const float* __restrict__ c0,
                                                           const float* __restrict__ keep,
                                                           const float* __restrict__ c_out,
@@ -96,6 +131,8 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const fl
                                                           const float* __restrict__ dh_n,
                                                           const float* __restrict__ dc_n, float* __restrict__ dxg,
                                                           float* __restrict__ dh0, float* __restrict__ dc0) {
+    constexpr int KU = UC > 0 ? UC : MAXU;
+    const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float dgs[4 * MAXU];
     __shared__ __attribute__((aligned(16))) float part[4 * MAXU];
     const int64_t b = blockIdx.x;
@@ -103,88 +140,130 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U, const fl
     const int G = 4 * U;
     // thread j < G is gate row j = q U + u in phase 1 (its gate's gradient) and, in phase 2,
     // sums quarter q of the gate rows for unit u: dh_prev'[u] = sum_r W_hh[r][u] dgates[r]
-    const int q = j / (U > 0 ? U : 1), u = j - q * U;
-    const bool act_j = j < G;
-    float wt[MAXU];
+    const bool act_j = (UC == MAXU) || j < G;
+    const int jc = act_j ? j : G - 1;
+    const int q = jc / U, u = jc - q * U;
+    float wt[KU];
 #pragma unroll
-    for (int m = 0; m < MAXU; ++m) wt[m] = (act_j && m < U) ? w_hh[(q * U + m) * U + u] : 0.0f;
+    for (int m = 0; m < KU; ++m) wt[m] = (act_j && m < U) ? w_hh[(q * U + m) * U + u] : 0.0f;
     // the recurrent gradients of unit u, kept (identically) by its four threads
     float dh_rec = (act_j && dh_n) ? dh_n[b * U + u] : 0.0f;
     float dc_rec = (act_j && dc_n) ? dc_n[b * U + u] : 0.0f;
-    // a step's saved activations / cells / output gradient of unit u, loaded one step ahead
+    // a step's saved activations / cells / output gradient of unit u (clamped addresses,
+    // unconditional loads; the t = 0 fix-ups are selects)
     struct StepIn {
         float ig, fg, gg, og, ct, cp, kprev, dh;
     };
-    auto load = [&](int t) {
-        StepIn v{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 1.f, 0.f};
-        if (act_j) {
-            const int64_t row = b * T + t;
-            const float* a = act + row * G;
-            v.ig = a[u];
-            v.fg = a[U + u];
-            v.gg = a[2 * U + u];
-            v.og = a[3 * U + u];
-            v.ct = c_out[row * U + u];
-            v.kprev = (t > 0 && keep) ? keep[row - 1] : 1.0f;
-            v.cp = t > 0 ? c_out[(row - 1) * U + u] : c0[b * U + u];
-            v.dh = dh_out[row * U + u];
-        }
+    const float c0u = c0[b * U + u];
+    auto load = [&](int t_raw) {
+        const int t = max(t_raw, 0);
+        const int64_t row = b * T + t;
+        const int64_t rp = t > 0 ? row - 1 : row;
+        StepIn v;
+        const float* a = act + row * G;
+        v.ig = a[u];
+        v.fg = a[U + u];
+        v.gg = a[2 * U + u];
+        v.og = a[3 * U + u];
+        v.ct = c_out[row * U + u];
+        const float kp = KEEP ? keep[rp] : 1.0f;
+        v.kprev = t > 0 ? kp : 1.0f;
+        const float cpv = c_out[rp * U + u];
+        v.cp = t > 0 ? cpv : c0u;
+        v.dh = dh_out[row * U + u];
         return v;
     };
-    StepIn nxt = load(T - 1);
+    StepIn cur[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) cur[p] = load(T - 1 - p);
     float k_after = 1.0f;   // keep between this step and the next one (applied to the parts)
     float dc_prev = 0.0f;
-    for (int t = T - 1; t >= 0; --t) {
-        const int64_t row = b * T + t;
-        const StepIn in = nxt;
-        if (t > 0) nxt = load(t - 1);
-        if (act_j) {
-            if (t < T - 1)   // dh_prev' of step t + 1, masked by the keep between t and t + 1
-                dh_rec = ((part[u] + part[U + u]) + (part[2 * U + u] + part[3 * U + u])) * k_after;
-            const float cp = t > 0 ? in.cp * in.kprev : in.cp;
-            const float dh = in.dh + dh_rec;
-            const float tc = tanhf(in.ct);
-            const float dc = dc_rec + dh * in.og * (1.0f - tc * tc);
-            float gq;
-            if (q == 0) gq = dc * in.gg * in.ig * (1.0f - in.ig);
-            else if (q == 1) gq = dc * cp * in.fg * (1.0f - in.fg);
-            else if (q == 2) gq = dc * in.ig * (1.0f - in.gg * in.gg);
-            else gq = dh * tc * in.og * (1.0f - in.og);
-            dgs[j] = gq;
-            dxg[row * G + j] = gq;
-            dc_prev = dc * in.fg;
-            dc_rec = dc_prev * in.kprev;
-            k_after = in.kprev;
-        }
-        __syncthreads();
-        if (act_j) {
-            float s0 = 0.0f, s1 = 0.0f;
-            if ((U & 3) == 0) {   // quarter rows start 16 B aligned: float4 reads (wt is 0 past U)
-                const float4* dg4 = reinterpret_cast<const float4*>(&dgs[q * U]);
+    for (int t0 = T - 1; t0 >= 0; t0 -= PB) {
+        StepIn nx[PB];
 #pragma unroll
-                for (int m = 0; m < MAXU; m += 4)
-                    if (m < U) {
-                        const float4 d = dg4[m / 4];
-                        s0 += wt[m] * d.x + wt[m + 2] * d.z;
-                        s1 += wt[m + 1] * d.y + wt[m + 3] * d.w;
-                    }
-            } else {
+        for (int p = 0; p < PB; ++p) nx[p] = load(t0 - PB - p);
 #pragma unroll
-                for (int m = 0; m < MAXU; m += 2)
-                    if (m < U) {
-                        s0 += wt[m] * dgs[q * U + m];
-                        if (m + 1 < U) s1 += wt[m + 1] * dgs[q * U + m + 1];
-                    }
+        for (int p = 0; p < PB; ++p) {
+            const int t = t0 - p;
+            if (t < 0) break;
+            const int64_t row = b * T + t;
+            const StepIn in = cur[p];
+            if (act_j) {
+                if (t < T - 1)   // dh_prev' of step t + 1, masked by the keep between t and t + 1
+                    dh_rec = ((part[u] + part[U + u]) + (part[2 * U + u] + part[3 * U + u])) * k_after;
+                const float cp = t > 0 ? in.cp * in.kprev : in.cp;
+                const float dh = in.dh + dh_rec;
+                const float tc = tanhf(in.ct);
+                const float dc = dc_rec + dh * in.og * (1.0f - tc * tc);
+                float gq;
+                if (q == 0) gq = dc * in.gg * in.ig * (1.0f - in.ig);
+                else if (q == 1) gq = dc * cp * in.fg * (1.0f - in.fg);
+                else if (q == 2) gq = dc * in.ig * (1.0f - in.gg * in.gg);
+                else gq = dh * tc * in.og * (1.0f - in.og);
+                dgs[j] = gq;
+                dxg[row * G + j] = gq;
+                dc_prev = dc * in.fg;
+                dc_rec = dc_prev * in.kprev;
+                k_after = in.kprev;
             }
-            part[j] = s0 + s1;
+            __syncthreads();
+            if (act_j) {
+                float s0 = 0.0f, s1 = 0.0f;
+                if ((U & 3) == 0) {   // quarter rows start 16 B aligned: float4 reads (wt is 0 past U)
+                    const float4* dg4 = reinterpret_cast<const float4*>(&dgs[q * U]);
+#pragma unroll
+                    for (int m = 0; m < KU; m += 4)
+                        if (UC > 0 || m < U) {
+                            const float4 d = dg4[m / 4];
+                            s0 += wt[m] * d.x + wt[m + 2] * d.z;
+                            s1 += wt[m + 1] * d.y + wt[m + 3] * d.w;
+                        }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < KU; m += 2)
+                        if (m < U) {
+                            s0 += wt[m] * dgs[q * U + m];
+                            if (m + 1 < U) s1 += wt[m + 1] * dgs[q * U + m + 1];
+                        }
+                }
+                part[j] = s0 + s1;
+            }
+            __syncthreads();
         }
-        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < PB; ++p) cur[p] = nx[p];
     }
     if (j < U) {
         if (dh0) dh0[b * U + j] = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
         if (dc0) dc0[b * U + j] = dc_prev;
     }
 }
+
+template <int UC, bool KEEP>
+void launch_fwd(int64_t n, int T, int U, const float* xg, const float* w_hh, const float* h0, const float* c0,
+                const float* keep, float* h_out, float* c_out, float* act, hipStream_t st) {
+    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
+}
+
+template <int UC, bool KEEP>
+void launch_bwd(int64_t n, int T, int U, const float* w_hh, const float* c0, const float* keep, const float* c_out,
+                const float* act, const float* dh_out, const float* dh_n, const float* dc_n, float* dxg, float* dh0,
+                float* dc0, hipStream_t st) {
+    lstm_seq_bwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n,
+                                                              dxg, dh0, dc0);
+}
+
+// the unit counts of the reference's configs (memory 128 -> 64, 64 -> 32, ...) compile
+// with constant trip counts; any other count runs the runtime-U instantiation
+#define SWARM_LSTM_DISPATCH(FN, KEEP, ...)                     \
+    switch (units) {                                            \
+    case 64: FN<64, KEEP>(__VA_ARGS__); break;                  \
+    case 32: FN<32, KEEP>(__VA_ARGS__); break;                  \
+    case 16: FN<16, KEEP>(__VA_ARGS__); break;                  \
+    case 8: FN<8, KEEP>(__VA_ARGS__); break;                    \
+    case 4: FN<4, KEEP>(__VA_ARGS__); break;                    \
+    default: FN<0, KEEP>(__VA_ARGS__); break;                   \
+    }
 
 bool args_ok(int64_t n, int32_t T, int32_t units) {
     return n >= 0 && n <= 0x7fffffff && T >= 1 && units >= 1 && units <= MAXU;
@@ -200,8 +279,12 @@ int32_t swarm_lstm_seq_forward(int64_t n, int32_t T, int32_t units, const float*
     if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
     if (n == 0) return SWARM_OK;
     if (!xg || !w_hh || !h0 || !c0 || !h_out || !c_out || !act) return SWARM_ERR_ARG;
-    lstm_seq_fwd_kernel<<<(unsigned)n, NT, 0, static_cast<hipStream_t>(stream)>>>(T, units, xg, w_hh, h0, c0, keep,
-                                                                                 h_out, c_out, act);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (keep) {
+        SWARM_LSTM_DISPATCH(launch_fwd, true, n, T, units, xg, w_hh, h0, c0, keep, h_out, c_out, act, st)
+    } else {
+        SWARM_LSTM_DISPATCH(launch_fwd, false, n, T, units, xg, w_hh, h0, c0, keep, h_out, c_out, act, st)
+    }
     return swarm::record_hip_status();
 }
 
@@ -212,8 +295,14 @@ int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float
     if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
     if (n == 0) return SWARM_OK;
     if (!w_hh || !c0 || !c_out || !act || !dh_out || !dxg) return SWARM_ERR_ARG;
-    lstm_seq_bwd_kernel<<<(unsigned)n, NT, 0, static_cast<hipStream_t>(stream)>>>(
-        T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0, dc0);
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (keep) {
+        SWARM_LSTM_DISPATCH(launch_bwd, true, n, T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0,
+                            dc0, st)
+    } else {
+        SWARM_LSTM_DISPATCH(launch_bwd, false, n, T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0,
+                            dc0, st)
+    }
     return swarm::record_hip_status();
 }
 

@@ -28,6 +28,11 @@ Tolerance (stated once, used by every parity test):
   * angles (yaw, the proximity / light angles of the sensor cache) are compared
     modulo 2*pi, and their spread is measured modulo 2*pi: yaw = atan2(sin, cos)
     (DG:826) maps a heading at +-pi to either end, both correct.
+  * the proximity aggregate (cache rows 0-1) is the vector sum of the 8 readings in
+    polar form; an angle that fails the rules above passes if the two aggregates
+    agree as vectors to 8 x 1e-5 (the readings' own bar): the angle of a nearly
+    cancelling sum (two opposite rays) is not determined beyond that. Counted with
+    the hull elements.
   * A discrete output may differ only where a 1-ulp perturbation of the
     oracle's inputs also changes it (a threshold sits within rounding).
   * `compare(..., stats=d)` counts the fp32 elements that pass only through the
@@ -207,6 +212,27 @@ def float_verdict(key: str, g, r, spread: dict | None):
     sp = None if spread is None else spread.get(key, 0.0)
     plain_ok = d <= plain
     ok = d <= tolerance(key, r, sp)
+    if spread is not None and key == "cache" and d.ndim >= 1 and d.shape[0] == 6 and not ok[1].all():
+        # The proximity aggregate (DG:114, ES:134-142) is the vector sum s of the 8 ray
+        # readings, cached in polar form: value min(1, |s|) (row 0), angle atan2(s) (row 1).
+        # Its angle is only as determined as the vector: readings within their 1e-5 bar
+        # leave s within 8e-5, i.e. the angle within 8e-5 / |s| (two opposite rays that
+        # nearly cancel give |s| ~ 1e-5). An angle element that fails the plain rule passes
+        # if the two aggregates agree as VECTORS to 8 x the readings' bar (+ the value's
+        # envelope); every such element is counted (`prox_vector_elements`).
+        g64, r64 = np.asarray(g, np.float64), np.asarray(r, np.float64)
+        vg = g64[0] * np.stack([np.cos(g64[1]), np.sin(g64[1])])
+        vr = r64[0] * np.stack([np.cos(r64[1]), np.sin(r64[1])])
+        sp0 = np.minimum(np.broadcast_to(np.asarray(sp if sp is not None else 0.0, np.float64), d.shape)[0],
+                         SPREAD_CAP)
+        vec_ok = np.sqrt(((vg - vr) ** 2).sum(0)) <= 8.0 * RTOL + SPREAD_FACTOR * sp0
+        extra = ~ok[1] & vec_ok & ok[0]
+        if extra.any():
+            ok = ok.copy()
+            ok[1] |= extra
+            hull_only = np.zeros(d.shape, bool)
+            hull_only[1] = extra
+            return ok, plain_ok, hull_only
     hull_only = np.zeros(d.shape, bool)
     if spread is not None and (key + "@base") in spread:
         ill = np.broadcast_to(np.asarray(sp), d.shape) > SPREAD_CAP
