@@ -54,8 +54,8 @@ def parse():
                     help="kernel work layout (4 = 4 waves share 3 arenas, 103 = 3 lanes per robot; 0 = library default)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline sample budget per leg (0 = skip)")
     ap.add_argument("--prewarm", type=float, default=1.0,
-                    help="seconds of untimed step launches on a scratch engine before the warm-up "
-                         "(brings the GPU to steady clocks; steps/warmup semantics unchanged)")
+                    help="seconds of untimed step launches on the timed engine before the warm-up "
+                         "(steady clocks, arenas past the post-spawn contact burst; steps/warmup unchanged)")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
@@ -102,10 +102,26 @@ def _oracle_worker(args):
             return E * N_AGENTS * steps, el
 
 
+CPU_SAMPLE_ENVS = (1, 64, 1024, 4096)   # the reference's CPU step at E = 1 / 64 / 1024 / 4096
+
+
+def _cpu_share() -> tuple[int, int]:
+    """(worker processes, CPUs in the affinity set). The GPU box's job share is the pool's
+    OMP_NUM_THREADS (16 per GPU there): its affinity set lists every CPU of the host
+    (256), but a pool larger than the share oversubscribes the job's quota, so the
+    all-cores leg runs one process per CPU of the share."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return max(1, min(aff, share)), aff
+
+
 def cpu_baseline(budget_s: float, envs: int) -> dict | None:
-    """Reference-equivalent CPU step (the C restatement in oracle/) on a bounded sample:
-    1 thread, then one process per host core (capped at the box's 16-core share),
-    each stepping its own slice of envs; the all-cores figure is `value`."""
+    """Reference-equivalent CPU step (the C restatement in oracle/) on bounded samples at
+    E = 1, 64, 1024, 4096 envs: 1 thread, then one process per CPU of the job's share, each
+    stepping its own slice of the E envs. `value` is the all-cores rate at the bench's E."""
     if budget_s <= 0:
         return None
     import multiprocessing as mp
@@ -113,24 +129,28 @@ def cpu_baseline(budget_s: float, envs: int) -> dict | None:
     from oracle import oracle as O
 
     O.build()
-    E = min(envs, 1024)
-    n1, el1 = _oracle_worker((E, budget_s, 0))
-    one = n1 / el1
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
-    per = max(1, E // cores)
+    cores, aff = _cpu_share()
+    sizes = sorted(set(CPU_SAMPLE_ENVS) | {envs})
+    per_leg = max(0.5, budget_s / (2 * len(sizes)))
+    table, value, one_at_e = [], None, None
     with mp.get_context("fork").Pool(cores) as pool:
-        res = pool.map(_oracle_worker, [(per, budget_s, 1 + k) for k in range(cores)])
-    allv = sum(n / el for n, el in res)
-    return {"value": allv, "unit": "agent-steps/s", "cores": cores, "kind": "port",
-            "one_thread": one, "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+        for E in sizes:
+            n1, el1 = _oracle_worker((E, per_leg, 0))
+            procs = max(1, min(cores, E))
+            res = pool.map(_oracle_worker, [(E // procs + (1 if k < E % procs else 0), per_leg, 1 + k)
+                                            for k in range(procs)])
+            allv = sum(n / el for n, el in res)
+            table.append({"envs": E, "one_thread": n1 / el1, "all_cores": allv, "processes": procs})
+            if E == envs:
+                value, one_at_e = allv, n1 / el1
+    return {"value": value, "unit": "agent-steps/s", "cores": cores, "kind": "port", "one_thread": one_at_e,
+            "by_envs": table, "cpu_model": _cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "affinity_cpus": aff,
             "sample": f"oracle/swarm_oracle.c (C restatement of the reference step, pinned by tests/golden) "
-                      f"Homing dandelion isaac profile, policy N(0,1)->clamp/3 per 5-step decision; "
-                      f"1 thread: {E} envs x 20 e-pucks for {el1:.1f} s = {one:.4g} agent-steps/s; "
-                      f"all cores: {cores} processes x {per} envs x 20 e-pucks for {budget_s:.0f} s each"}
+                      f"Homing dandelion isaac profile, policy N(0,1)->clamp/3 per 5-step decision, "
+                      f"E in {list(sizes)} envs x 20 e-pucks, {per_leg:.1f} s per leg: 1 thread, then "
+                      f"{cores} processes (the job's CPU share; the affinity set lists {aff}) each stepping "
+                      f"E / {cores} envs; value = all-cores rate at E = {envs}"}
 
 
 def load_pmc(envs: int, sub: int) -> dict:
@@ -148,16 +168,13 @@ def load_pmc(envs: int, sub: int) -> dict:
     return d
 
 
-def prewarm(seconds: float, E: int, dp: int, dev) -> float:
-    """Untimed launches of the same workload (same step, same action distribution) on a
-    scratch engine for `seconds`, run right before the warm-up decisions so the clocks
-    are up when the timed region starts."""
+def prewarm(seconds: float, eng, E: int, dp: int, dev, out) -> float:
+    """Untimed launches of the same workload (same step, same action distribution) on the
+    timed engine itself for `seconds`, right before the warm-up decisions: the clocks are
+    up and the arenas are past the contact burst that follows a spawn when the timed
+    region starts, however few launches it has."""
     if seconds <= 0:
         return 0.0
-    from SwarmACB_isaac.engine import SwarmEngine
-
-    eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, 0, 12345, dev)
-    out = eng.reset()
     g = torch.Generator(device=dev).manual_seed(12345)
     acts = (torch.randn(8, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
     t0 = time.perf_counter()
@@ -167,7 +184,6 @@ def prewarm(seconds: float, E: int, dp: int, dev) -> float:
             eng.step(acts[i % 8], dp, out=out)
             i += 1
         torch.cuda.synchronize(dev)
-    eng.close()
     return time.perf_counter() - t0
 
 
@@ -228,7 +244,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
     acts = (torch.randn(n_warm + n_dec, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
 
-    prewarm_s = prewarm(args.prewarm, E, dp, dev)
+    prewarm_s = prewarm(args.prewarm, eng, E, dp, dev, out)
     for d in range(n_warm):
         eng.step(acts[d], dp, out=out)
     torch.cuda.synchronize(dev)
@@ -243,6 +259,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    # a short device-side spin ahead of the start event keeps the GPU busy while the host
+    # enqueues the event and the first launches, so the event region holds the launches
+    # back to back (no first-launch host latency inside the kernel average)
+    torch.cuda._sleep(10000)
     ev0.record(stream)
     for d in range(n_dec):
         eng.step(acts[n_warm + d], dp, out=out)

@@ -27,6 +27,12 @@ import torch
 
 # SWARM_GRAPHS=0 forces eager steps
 ENABLED = os.environ.get("SWARM_GRAPHS", "1") != "0"
+# SWARM_GRAPHS_DIST=1 also captures multi-rank steps on the RCCL ("nccl") backend: the
+# flat-gradient all-reduce and the loss-denominator all-reduces go into the graph (RCCL
+# collectives are stream-ordered and capturable; gloo's host round trips are not). Off by
+# default: a captured collective cannot be validated without two GPUs (RCCL refuses two
+# ranks on one device), and a capture that fails falls back to eager steps anyway.
+DIST_ENABLED = os.environ.get("SWARM_GRAPHS_DIST", "0") == "1"
 
 
 def make_capturable(optimizers, device: torch.device):

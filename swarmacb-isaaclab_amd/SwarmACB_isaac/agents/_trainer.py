@@ -162,9 +162,10 @@ class TrainerBase:
 
     # ------------------------------------------------------------ graphed steps
     def _graphs_ok(self) -> bool:
-        """Replay optimizer steps from a HIP graph (agents/_graph.py): single process on
-        a ROCm device, no per-step test hooks."""
-        return (_graph.ENABLED and self.device.type == "cuda" and not self.comm.active
+        """Replay optimizer steps from a HIP graph (agents/_graph.py): a ROCm device, no
+        per-step test hooks, one process (or RCCL ranks with SWARM_GRAPHS_DIST=1)."""
+        dist_ok = not self.comm.active or (_graph.DIST_ENABLED and self.comm.backend == "nccl")
+        return (_graph.ENABLED and self.device.type == "cuda" and dist_ok
                 and self.grad_hook is None and self.step_hook is None)
 
     def _step_runner(self, step_fn, optimizers):

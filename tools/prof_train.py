@@ -43,6 +43,11 @@ def main():
     tr.update()
     torch.cuda.synchronize()
     tr._sequence_batches = lambda: itertools.islice(orig(), a.steps)
+    if os.environ.get("PROF_TRAIN_NOPROF"):
+        # under rocprofv3: the same optimizer steps without the torch profiler
+        tr.update()
+        torch.cuda.synchronize()
+        return
     from torch.profiler import ProfilerActivity, profile
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
         tr.update()
