@@ -259,10 +259,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    # a short device-side spin ahead of the start event keeps the GPU busy while the host
-    # enqueues the event and the first launches, so the event region holds the launches
-    # back to back (no first-launch host latency inside the kernel average)
-    torch.cuda._sleep(10000)
     ev0.record(stream)
     for d in range(n_dec):
         eng.step(acts[n_warm + d], dp, out=out)

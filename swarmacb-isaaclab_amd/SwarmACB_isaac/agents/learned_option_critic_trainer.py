@@ -383,11 +383,11 @@ class LearnedOptionCriticTrainer(TrainerBase):
         new_action_bl = self.action_critic.focal_baselines(option_states, flat_joint_actions, focal_ids,
                                                            mem("action_baseline_memory"),
                                                            sequence_length=L).squeeze(-1)
-        new_joint = self.option_critic.joint_action_pass(flat_states, encoded, mem("option_joint_memory"),
-                                                         sequence_length=L).squeeze(-1)
-        new_option_bl = self.option_critic.focal_baselines(flat_states, encoded, focal_ids,
-                                                           mem("option_baseline_memory"),
-                                                           sequence_length=L).squeeze(-1)
+        # the option critic's joint_action_pass and focal_baselines as one batched pass
+        new_joint, new_option_bl = self.option_critic.sequence_passes(
+            flat_states, encoded, focal_ids,
+            {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")},
+            sequence_length=L, passes=("joint", "baseline"))
 
         def tr_loss(new, old_key):
             return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,

@@ -168,12 +168,13 @@ class FixedOptionCriticTrainer(TrainerBase):
         def mem(k):
             return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
 
-        new_team_values = self.critic.critic_pass(flat_states, mem("value_memory"), sequence_length=L).squeeze(-1)
-        new_joint = self.critic.joint_action_pass(flat_states, critic_options, mem("joint_memory"),
-                                                  sequence_length=L).squeeze(-1)
+        # critic_pass, joint_action_pass and focal_baselines (OCT:571-608) as one batched pass
+        # (POCACritic.sequence_passes)
         focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        new_baselines = self.critic.focal_baselines(flat_states, critic_options, focal_ids, mem("baseline_memory"),
-                                                    sequence_length=L).squeeze(-1)
+        new_team_values, new_joint, new_baselines = self.critic.sequence_passes(
+            flat_states, critic_options, focal_ids,
+            {"value": mem("value_memory"), "joint": mem("joint_memory"), "baseline": mem("baseline_memory")},
+            sequence_length=L, passes=("value", "joint", "baseline"))
         value_loss = trust_region_value_loss(new_team_values, batch["old_team_values"].reshape(B * L), flat_returns,
                                              current_eps, flat_loss_mask, denom=d_mask)
         joint_loss = trust_region_value_loss(new_joint, batch["old_joint_option_values"].reshape(B * L),

@@ -568,6 +568,50 @@ class POCACritic(nn.Module):
                              all_actions.gather(1, others.expand(B, N - 1, all_actions.shape[-1])), memory,
                              sequence_length, return_memory)
 
+    def _focal_entities(self, all_states, all_actions, focal_agent_ids):
+        """The baseline set of each row's focal agent (poca_networks.py:764-820): its state-only
+        entity, then the other agents' state+action entities in increasing order (by index,
+        no boolean-mask select: other k = k + (k >= focal))."""
+        B, N, _ = all_states.shape
+        rows = torch.arange(B, device=all_states.device)
+        focal = focal_agent_ids.long()
+        k = torch.arange(N - 1, device=all_states.device).unsqueeze(0)
+        others = (k + (k >= focal.unsqueeze(1)).long()).unsqueeze(-1)
+        o_states = all_states.gather(1, others.expand(B, N - 1, all_states.shape[-1]))
+        o_actions = all_actions.gather(1, others.expand(B, N - 1, all_actions.shape[-1]))
+        return torch.cat([self.obs_entity_enc(all_states[rows, focal].unsqueeze(1)),
+                          self.obs_act_entity_enc(torch.cat([o_states, o_actions], dim=-1))], dim=1)
+
+    def sequence_passes(self, all_states, all_actions, focal_agent_ids, memories: dict, sequence_length: int,
+                        passes=("value", "baseline")):
+        """Several of the critic's training-time passes over the same rows as ONE batched pass:
+        "value" = critic_pass(states), "joint" = joint_action_pass(states, actions), "baseline" =
+        focal_baselines(states, actions, focal) (poca_trainer.py:748-770, option_critic_trainer.py:
+        571-608), each with its own memory (memories[name] = (h, c) of shape (1, sequences, units)).
+        Every op of a pass is per set row (self-attention within a set, row-wise encoder and head)
+        or per sequence (the LSTM), so stacking the passes along the batch gives each pass's values
+        unchanged (up to GEMM summation order): one attention, one encoder, ONE LSTM launch over
+        all passes' sequences and one head instead of one of each per pass. Returns the (B,)
+        values of each pass in `passes` order."""
+        B, N, _ = all_states.shape
+        sets = []
+        for name in passes:
+            if name == "value":
+                sets.append(self.obs_entity_enc(all_states))
+            elif name == "joint":
+                sets.append(self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1)))
+            elif name == "baseline":
+                sets.append(self._focal_entities(all_states, all_actions, focal_agent_ids))
+            else:
+                raise ValueError(f"unknown critic pass {name!r}")
+        ents = torch.cat(sets, dim=0)
+        memory = None
+        if self.lstm is not None:
+            memory = tuple(torch.cat([memories[name][i] for name in passes], dim=1) for i in (0, 1))
+        pooled = self.self_attn(ents)
+        values = self._value_tail(pooled, N, memory, sequence_length).squeeze(-1)
+        return list(values.split(B))
+
     def decision_passes(self, all_states, all_actions, *, value: bool = True, joint: bool = False,
                         baselines: bool = True, value_memory=None, joint_memory=None, baseline_memory=None):
         """The per-decision critic calls of the trainers' rollouts on ONE decision's entities:

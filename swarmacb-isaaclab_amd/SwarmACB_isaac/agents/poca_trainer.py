@@ -168,13 +168,13 @@ class POCATrainer(TrainerBase):
         flat_actions = batch["critic_actions"].reshape(B * L, N, batch["critic_actions"].shape[-1])
         critic_act = self._encode_actions_for_critic(flat_actions)
         focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        new_tv = self.critic.critic_pass(
-            flat_states, (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
-            sequence_length=L).squeeze(-1)
-        new_bl = self.critic.focal_baselines(
+        # critic_pass and focal_baselines (PT:748-770) as one batched pass (POCACritic.sequence_passes)
+        new_tv, new_bl = self.critic.sequence_passes(
             flat_states, critic_act, focal_ids,
-            (batch["baseline_memory_h"].unsqueeze(0).detach(), batch["baseline_memory_c"].unsqueeze(0).detach()),
-            sequence_length=L).squeeze(-1)
+            {"value": (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
+             "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
+                          batch["baseline_memory_c"].unsqueeze(0).detach())},
+            sequence_length=L, passes=("value", "baseline"))
         flat_mask = loss_mask.reshape(B * L)
         value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
                                              batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)

@@ -35,31 +35,50 @@ __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(
 constexpr int PF = 8;
 constexpr int PB = 4;
 
+// Activations from the hardware exponential and reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp
+// each) instead of the library's expf / tanhf / IEEE division, which dominated the
+// per-step chain; tanh(x) = 2 sigmoid(2x) - 1 (absolute error ~1e-7 near 0).
+__device__ __forceinline__ float fast_sigmoid(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigmoid(2.0f * x) - 1.0f; }
+
+// Forward: NF = 512 threads = 8 waves per sequence. Gate row j = t >> 1 is split over two
+// adjacent lanes (each a half of the U-long dot product with h, one DPP add joins them), so
+// a step's products are 2 waves per SIMD deep instead of one 64-long chain per lane. The
+// gates of a step go through ONE LDS buffer (double-buffered by step parity) and ONE
+// barrier; then every wave computes all U cell updates itself (lane u = unit u) and keeps
+// h in its own LDS row, so the next step's products need no second barrier.
+constexpr int NF = 512;
+
 template <int UC, bool KEEP>
-__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
+__global__ void __launch_bounds__(NF) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
                                                           const float* __restrict__ w_hh,
                                                           const float* __restrict__ h0,
                                                           const float* __restrict__ c0,
                                                           const float* __restrict__ keep, float* __restrict__ h_out,
                                                           float* __restrict__ c_out, float* __restrict__ act) {
     constexpr int KU = UC > 0 ? UC : MAXU;              // register extent of a gate row
+    constexpr int KH = (KU + 1) / 2;                     // per half-lane
     const int U = UC > 0 ? UC : U_rt;
-    __shared__ __attribute__((aligned(16))) float hs[MAXU];
-    __shared__ float gs[4 * MAXU];
+    const int UH = (U + 1) / 2;
+    __shared__ __attribute__((aligned(16))) float hs[NF / 64][MAXU];   // per-wave copy of h
+    __shared__ __attribute__((aligned(16))) float gs[2][4 * MAXU];
     const int64_t b = blockIdx.x;
-    const int j = threadIdx.x;
+    const int t_id = threadIdx.x;
+    const int wave = t_id >> 6, lane = t_id & 63;
     const int G = 4 * U;
-    const bool row_j = (UC == MAXU) || j < G;           // thread j owns gate pre-activation j
-    const int jc = row_j ? j : G - 1;                    // clamped: loads never leave the row
-    float w[KU];
+    const int j = t_id >> 1, half = t_id & 1;
+    const bool row_j = j < G;
+    const int jc = row_j ? j : G - 1;
+    const int k0 = half * UH;                            // this lane's half of the dot product
+    float w[KH];
 #pragma unroll
-    for (int k = 0; k < KU; ++k) w[k] = (row_j && k < U) ? w_hh[jc * U + k] : 0.0f;
-    float c = 0.0f;
-    if (j < MAXU) hs[j] = j < U ? h0[b * U + j] : 0.0f;   // padded to a multiple of 4 for float4 reads
-    if (j < U) c = c0[b * U + j];
-    const int kind = j / U;                              // 0 i, 1 f, 2 g, 3 o
-    // inputs of step t: the gate pre-activation x W_ih^T + b and the keep applied to
-    // the state carried into t + 1 (1 after the last step)
+    for (int k = 0; k < KH; ++k) w[k] = (row_j && k < UH && k0 + k < U) ? w_hh[jc * U + k0 + k] : 0.0f;
+    const bool unit = lane < U;                          // lane u = unit u in every wave
+    float c = unit ? c0[b * U + lane] : 0.0f;
+    hs[wave][lane] = unit ? h0[b * U + lane] : 0.0f;
+    const int kind = jc / U;                             // 0 i, 1 f, 2 g, 3 o
     const float* xb = xg + b * T * G + jc;
     auto load_group = [&](int t0, float* xr, float* kr) {
 #pragma unroll
@@ -71,7 +90,8 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
     };
     float xr[PF], kr[PF] = {};
     load_group(0, xr, kr);
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int t0 = 0; t0 < T; t0 += PF) {
         float xn[PF], kn[PF] = {};
         load_group(t0 + PF, xn, kn);
@@ -80,38 +100,49 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
             const int t = t0 + p;
             if (t >= T) break;
             const int64_t row = b * T + t;
-            if (row_j) {
-                // four independent accumulation chains (16 deep at 64 units)
+            float* g = gs[t & 1];
+            {
+                const float* h = &hs[wave][k0];
                 float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+                if constexpr (UC > 0 && KH % 4 == 0) {
 #pragma unroll
-                for (int k = 0; k < KU; k += 8)
-                    if (UC > 0 || k < U) {
-                        const float4 h4 = *reinterpret_cast<const float4*>(&hs[k]);
-                        a0 += w[k] * h4.x + w[k + 2] * h4.z;
-                        a1 += w[k + 1] * h4.y + w[k + 3] * h4.w;
-                        if (k + 4 < KU && (UC > 0 || k + 4 < U)) {
-                            const float4 g4 = *reinterpret_cast<const float4*>(&hs[k + 4]);
-                            a2 += w[k + 4] * g4.x + w[k + 6] * g4.z;
-                            a3 += w[k + 5] * g4.y + w[k + 7] * g4.w;
-                        }
+                    for (int k = 0; k < KH; k += 4) {
+                        const float4 h4 = *reinterpret_cast<const float4*>(h + k);
+                        a0 += w[k] * h4.x;
+                        a1 += w[k + 1] * h4.y;
+                        a2 += w[k + 2] * h4.z;
+                        a3 += w[k + 3] * h4.w;
                     }
-                const float a = ((a0 + a1) + (a2 + a3)) + xr[p];
-                const float v = kind == 2 ? tanhf(a) : sigmoidf(a);
-                gs[j] = v;
-                act[row * G + j] = v;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < KH; ++k)
+                        if (k < UH) a0 += w[k] * h[k];
+                }
+                float a = (a0 + a1) + (a2 + a3);
+                a += __shfl_xor(a, 1);                   // the other half of row j
+                if (row_j && half == 0) {
+                    a += xr[p];
+                    const float v = kind == 2 ? fast_tanh(a) : fast_sigmoid(a);
+                    g[j] = v;
+                    act[row * G + j] = v;
+                }
             }
             __syncthreads();
-            if (j < U) {
-                c = gs[U + j] * c + gs[j] * gs[2 * U + j];
-                const float h = gs[3 * U + j] * tanhf(c);
-                h_out[row * U + j] = h;
-                c_out[row * U + j] = c;
+            if (unit) {
+                c = g[U + lane] * c + g[lane] * g[2 * U + lane];
+                const float h = g[3 * U + lane] * fast_tanh(c);
+                if (wave == 0) {
+                    h_out[row * U + lane] = h;
+                    c_out[row * U + lane] = c;
+                }
                 // the state carried into step t + 1 is masked where the episode ended at t
                 const float kk = (KEEP && t + 1 < T) ? kr[p] : 1.0f;
-                hs[j] = h * kk;
+                hs[wave][lane] = h * kk;
                 c *= kk;
             }
-            __syncthreads();
+            // h is read back by this wave only: wave-scope ordering, no barrier
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
@@ -242,7 +273,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
 template <int UC, bool KEEP>
 void launch_fwd(int64_t n, int T, int U, const float* xg, const float* w_hh, const float* h0, const float* c0,
                 const float* keep, float* h_out, float* c_out, float* act, hipStream_t st) {
-    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
+    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NF, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
 }
 
 template <int UC, bool KEEP>

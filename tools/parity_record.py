@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Aggregate the per-test parity statistics of a `pytest -m gpu` run
+(gpurun_out/parity_stats.jsonl, written by tests/parity.py record_stats) into the
+committed envelope record: per group and per test, how many fp32 elements passed only
+through the 1-ulp conditioning envelope (and the largest |delta| among them, per key),
+how many only through the hull rule for ill-conditioned elements (with examples), and
+how many discrete elements were exempted as unstable.
+
+Usage: python tools/parity_record.py gpurun_out/parity_stats.jsonl profiles/r03/parity_envelope.json
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+
+
+def main(src: str, dst: str, note: str = ""):
+    rows = [json.loads(line) for line in open(src) if line.strip()]
+    groups: dict = {}
+    for r in rows:
+        g = groups.setdefault(r["test"].split("/")[0], {"tests": 0, "envelope_max_delta": {}, "hull_examples": []})
+        g["tests"] += 1
+        for k, v in r.items():
+            if k == "test":
+                continue
+            if isinstance(v, dict):
+                for kk, vv in v.items():
+                    g["envelope_max_delta"][kk] = max(g["envelope_max_delta"].get(kk, 0.0), vv)
+            elif isinstance(v, list):
+                g["hull_examples"] += [dict(e, test=r["test"]) for e in v][:max(0, 16 - len(g["hull_examples"]))]
+            else:
+                g[k] = g.get(k, 0) + v
+    rec = {
+        "source": note or f"pytest -m gpu on MI355X (tests/parity.py record_stats), {src}",
+        "rule": ("discrete outputs exact unless a 1-ulp input perturbation flips them; fp32 |got-ref| <= "
+                 "1e-5*scale + 4*min(spread, 1e-3); elements with spread > 1e-3 (a discontinuity or sqrt "
+                 "singularity within one ulp) may instead pass if both values lie in the hull of the oracle's "
+                 "perturbed outputs (+-1e-5*scale); the proximity aggregate angle may pass as a vector "
+                 "(8e-5); angles mod 2 pi"),
+        "groups": groups,
+        "per_test": rows,
+    }
+    with open(dst, "w") as f:
+        json.dump(rec, f, indent=1)
+    for name, g in groups.items():
+        print(name, {k: v for k, v in g.items() if k != "hull_examples"}, f"{len(g['hull_examples'])} hull examples")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
