@@ -72,7 +72,7 @@ class FixedOptionCriticTrainer(TrainerBase):
         self.critic = POCACritic(self.state_dim, c.num_options, self.num_agents, c.critic_hidden_dim,
                                  c.critic_num_heads, c.critic_num_layers, memory_size=c.memory_size).to(self.device)
         self.params = list(self.manager.parameters()) + list(self.critic.parameters())
-        self.optimizer = optim.Adam(self.params, lr=c.lr, eps=c.adam_eps)
+        self.optimizer = optim.Adam(self.params, lr=c.lr, eps=c.adam_eps, fused=self.device.type == "cuda")
         self.comm.bind_flat_grads(self.params)
 
         self.buffer = FixedOptionRolloutBuffer(

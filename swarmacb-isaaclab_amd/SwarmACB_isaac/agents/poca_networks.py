@@ -35,12 +35,62 @@ _KERNEL_INITS = {
 }
 
 
+SPLITK_MIN_ROWS = 8192     # rows from which a layer's weight gradient is split over row chunks
+SPLITK_CHUNK_ROWS = 1024   # rows per chunk of that split
+
+
+class _SplitKLinear(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient dW = dy^T x sums over R >= SPLITK_MIN_ROWS
+    rows (the critic's entity rows: every env x agent x entity of a minibatch). As one
+    GEMM that is an (out x in) output with a 40k-deep reduction: a dozen output tiles,
+    i.e. a dozen busy CUs of 256. Split into R / SPLITK_CHUNK_ROWS row chunks it is one
+    batched GEMM with hundreds of tiles plus a sum over the chunks (fp32 sums in another
+    order; the forward and dx are the plain GEMMs)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.addmm(bias, x, weight.t()) if bias is not None else x.mm(weight.t())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = dy.mm(weight) if ctx.needs_input_grad[0] else None
+        R = x.shape[0]
+        c = R // SPLITK_CHUNK_ROWS
+        L = R // c
+        main = c * L
+        dyc = dy[:main].view(c, L, dy.shape[1])
+        dw = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1])).sum(dim=0)
+        db = dyc.sum(dim=1).sum(dim=0) if ctx.has_bias else None
+        if main < R:
+            dw.addmm_(dy[main:].t(), x[main:])
+            if db is not None:
+                db += dy[main:].sum(dim=0)
+        return dx, dw, db
+
+
+class _Linear(nn.Linear):
+    """nn.Linear (same parameters and state-dict keys) whose GPU calls over at least
+    SPLITK_MIN_ROWS rows take the split-row weight gradient of _SplitKLinear."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32):
+            return super().forward(x)
+        rows = x.numel() // x.shape[-1] if x.dim() else 0
+        if rows < SPLITK_MIN_ROWS:
+            return super().forward(x)
+        y = _SplitKLinear.apply(x.reshape(rows, x.shape[-1]), self.weight, self.bias)
+        return y.view(*x.shape[:-1], self.out_features)
+
+
 def _linear_layer(input_size: int, output_size: int, kernel_init: str = "xavier_uniform",
                   kernel_gain: float = 1.0, bias_init: str = "zeros") -> nn.Linear:
     """ML-Agents-initialised linear layer (poca_networks.py:58-82)."""
     if kernel_init not in _KERNEL_INITS:
         raise ValueError(f"Unknown kernel_init: {kernel_init}")
-    layer = nn.Linear(input_size, output_size)
+    layer = _Linear(input_size, output_size)
     _KERNEL_INITS[kernel_init](layer.weight)
     layer.weight.data *= kernel_gain
     if bias_init == "zeros":
@@ -371,7 +421,11 @@ class ResidualSelfAttention(nn.Module):
             # core of every set and head in one MFMA kernel each way (_AttnCore)
             w = torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight])
             b = torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias])
-            qkv = torch.nn.functional.linear(x.reshape(B * N, D), w, b).contiguous()
+            x2 = x.reshape(B * N, D)
+            if torch.is_grad_enabled() and B * N >= SPLITK_MIN_ROWS:
+                qkv = _SplitKLinear.apply(x2, w, b)
+            else:
+                qkv = torch.nn.functional.linear(x2, w, b).contiguous()
             km = key_mask.reshape(B, N).to(torch.float32).contiguous() if key_mask is not None else None
             att = _AttnCore.apply(qkv, km, B, N, H).view(B, N, D)
         else:

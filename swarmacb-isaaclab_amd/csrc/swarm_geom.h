@@ -32,6 +32,8 @@ enum RngPurpose : uint32_t {
     S(int32_t, apb)      /* arenas per 64-lane wave (= 64 / N) */                                            \
     S(int32_t, layout)   /* work layout LY (swarm_step_impl.h): 1, 4 or 103 */                               \
     S(uint32_t, seed_lo) S(uint32_t, seed_hi) S(uint32_t, env_off_lo) S(uint32_t, env_off_hi)               \
+    S(int32_t, env0)     /* first arena of this step launch (env groups on separate streams, swarm_capi.cpp) */ \
+    S(int32_t, env_n)    /* arenas of this step launch (0 = all E) */                                        \
     /* ---- mission constants (compile time in the kernels) ---- */                                          \
     S(int32_t, nseg) S(int32_t, nint) /* raycast segments (arena 12 + internal), internal walls */           \
     S(int32_t, has_light)                                                                                   \

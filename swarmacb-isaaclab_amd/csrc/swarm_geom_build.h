@@ -33,6 +33,8 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     g.seed_hi = (uint32_t)(p.seed >> 32);
     g.env_off_lo = (uint32_t)p.env_offset;
     g.env_off_hi = (uint32_t)((uint64_t)p.env_offset >> 32);
+    g.env0 = 0;
+    g.env_n = 0;
 
     // arena: regular dodecagon of area 4.91 m^2 (DGC:32-36, DG:615-628)
     const int n = 12;

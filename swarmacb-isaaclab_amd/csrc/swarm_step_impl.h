@@ -1524,7 +1524,7 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime k
     const int chunk = (L.N + P - 1) / P;
     L.j0 = L.p * chunk;
     L.j1 = min(L.N, L.j0 + chunk);
-    L.env = blockIdx.x * apb + L.a;
+    L.env = g.env0 + (int)blockIdx.x * apb + L.a;
     L.valid = (L.a < apb) && (L.env < g.E);
     L.ab = (L.a < apb ? L.a : 0) * L.N;
     // lanes beyond the last whole arena own no robot: park their tile writes in
@@ -1837,7 +1837,7 @@ static void launch_step_t(const Geom& g, const DevState& st, const void* act, co
                                stream, g, st, act, ovr, out, rp, tick, n_sub, reset_any);                             \
     } while (0)
     if (g.layout == 103) {   // one arena per wave, 3 lanes per robot (N <= 21, checked by swarm_create)
-        const int blocks = g.E;
+        const int blocks = g.env_n > 0 ? g.env_n : g.E;   // arenas [env0, env0 + blocks)
         if (g.N == 20)
             SWARM_LAUNCH_STEP(20, 103);
         else
