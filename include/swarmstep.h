@@ -143,6 +143,15 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
                    const float* override_wheels, const swarm_outputs_t* out, int32_t n_substeps,
                    const swarm_replay_t* replay, void* stream);
 
+/* Split every later swarm_step launch into `groups` contiguous env ranges (1..8, at most E),
+ * each launched on a stream the handle owns and joined back to the caller's stream with events
+ * (stream-ordered and graph-capturable; results are bitwise those of one launch: arenas are
+ * independent and every draw is keyed by global env). A step launch lasts as long as its slowest
+ * arena; with groups, one range's tail overlaps the others' launches. Creates the streams on the
+ * current device. 1 = one launch on the caller's stream (the default). Layout 103 only (others
+ * ignore it). No reference counterpart: a scheduling knob of this library. */
+int32_t swarm_set_step_groups(swarm_handle_t* h, int32_t groups);
+
 /* get_critic_state() (directional_gate_env.py:1279-1290 -> epuck_sensors.py:545-586): out [E*N*5]. */
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream);
 

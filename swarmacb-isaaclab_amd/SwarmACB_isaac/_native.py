@@ -51,7 +51,7 @@ class SwarmReplay(C.Structure):
 EXPORTS = [
     "swarm_abi_version", "swarm_strerror", "swarm_last_hip_error", "swarm_create", "swarm_destroy",
     "swarm_reset", "swarm_step", "swarm_critic_state", "swarm_sync_episode_lengths", "swarm_tick",
-    "swarm_last_timeouts",
+    "swarm_last_timeouts", "swarm_set_step_groups",
     "swarm_fsm_pack",
 ]
 
@@ -126,6 +126,8 @@ def load() -> C.CDLL:
     lib.swarm_tick.argtypes = [C.c_void_p]
     lib.swarm_last_timeouts.restype = C.c_int64
     lib.swarm_last_timeouts.argtypes = [C.c_void_p]
+    lib.swarm_set_step_groups.restype = C.c_int32
+    lib.swarm_set_step_groups.argtypes = [C.c_void_p, C.c_int32]
     lib.swarm_fsm_pack.restype = C.c_uint32
     lib.swarm_fsm_pack.argtypes = [C.c_int32, C.c_int32, C.c_float] * 3
     i32, i64, vp = C.c_int32, C.c_int64, C.c_void_p

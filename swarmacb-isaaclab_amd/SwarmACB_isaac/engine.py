@@ -59,7 +59,8 @@ class SwarmEngine:
 
     def __init__(self, mission: str, profile: str = "isaac", num_envs: int = 1, num_agents: int = 20,
                  obs_dim: int = 24, discrete: bool = False, max_episode_length: int = 1200,
-                 decimation: int = 1, env_offset: int = 0, seed: int = 0, device="cuda:0", layout: int | None = None):
+                 decimation: int = 1, env_offset: int = 0, seed: int = 0, device="cuda:0", layout: int | None = None,
+                 step_groups: int | None = None):
         self.lib = _native.load()
         self.device = torch.device(device)
         if self.device.type != "cuda":
@@ -76,6 +77,7 @@ class SwarmEngine:
         h = C.c_void_p()
         _native.check(self.lib.swarm_create(C.byref(self.params), C.byref(h)), "swarm_create")
         self.handle = h
+        self.set_step_groups(step_groups if step_groups is not None else int(os.environ.get("SWARM_STEP_GROUPS", 1)))
         E, N, dev = self.E, self.N, self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.x = torch.zeros(E * N, **f32)
@@ -94,6 +96,15 @@ class SwarmEngine:
         self._state = _native.SwarmState(*[t.data_ptr() for t in (
             self.x, self.y, self.yaw, self.fsm, self.wheel_l, self.wheel_r, self.cache, self.ground_prev,
             self.flags, self.episode_length, self.episode_reward, self.completed_reward, self.terminal_critic)])
+
+    def set_step_groups(self, groups: int):
+        """Launch each step as `groups` env ranges on streams of their own, joined back to the
+        current stream (swarm_set_step_groups, include/swarmstep.h): a range's slowest arena
+        no longer holds the others' SIMDs idle. Bitwise the same results."""
+        groups = max(1, min(int(groups), self.E))
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.swarm_set_step_groups(self.handle, groups), "swarm_set_step_groups")
+        self.step_groups = groups
 
     # ------------------------------------------------------------------ calls
     def _stream(self):

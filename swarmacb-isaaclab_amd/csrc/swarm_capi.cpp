@@ -28,6 +28,7 @@ using namespace swarm;
 
 namespace {
 
+constexpr int SWARM_MAX_STEP_GROUPS = 8;
 thread_local int32_t g_last_hip = 0;
 
 // Histogram of episode lengths stored relative to a global offset: all envs
@@ -68,15 +69,21 @@ struct swarm_handle {
     std::vector<int32_t> lens;  // per-env host copy, refreshed lazily
     bool lens_exact = true;     // lens[] matches the mirror
     uint8_t* d_mask = nullptr;  // E-byte device scratch for reset masks
+    uint8_t* d_cost = nullptr;  // E-byte per-arena solver work of the last step launch (scheduling hint)
     bool was_reset = false;
     uint64_t last_timeouts = 0;  // substeps of the last swarm_step in which some env timed out
+    // env groups of swarm_set_step_groups: one owned stream + join event per group
+    int groups = 1;
+    hipStream_t gstream[SWARM_MAX_STEP_GROUPS] = {};
+    hipEvent_t gjoin[SWARM_MAX_STEP_GROUPS] = {};
+    hipEvent_t gfork = nullptr;
 };
 
 namespace {
 
 DevState dev_state(const swarm_state_t* s) {
     return DevState{s->pos_x, s->pos_y, s->yaw, s->fsm, s->wheel_l, s->wheel_r, s->sensor_cache, s->ground_prev,
-                    s->flags, s->episode_length, s->episode_reward, s->completed_reward, s->terminal_critic};
+                    s->flags, s->episode_length, s->episode_reward, s->completed_reward, s->terminal_critic, nullptr};
 }
 
 bool state_ok(const swarm_state_t* s) {
@@ -154,9 +161,42 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     return SWARM_OK;
 }
 
+namespace {
+void free_groups(swarm_handle_t* h) {
+    for (int k = 0; k < SWARM_MAX_STEP_GROUPS; ++k) {
+        if (h->gstream[k]) (void)hipStreamDestroy(h->gstream[k]);
+        if (h->gjoin[k]) (void)hipEventDestroy(h->gjoin[k]);
+        h->gstream[k] = nullptr;
+        h->gjoin[k] = nullptr;
+    }
+    if (h->gfork) (void)hipEventDestroy(h->gfork);
+    h->gfork = nullptr;
+    h->groups = 1;
+}
+}  // namespace
+
+int32_t swarm_set_step_groups(swarm_handle_t* h, int32_t groups) {
+    if (!h || groups < 1 || groups > SWARM_MAX_STEP_GROUPS || groups > h->p.num_envs) return SWARM_ERR_ARG;
+    free_groups(h);
+    if (groups == 1) return SWARM_OK;
+    bool ok = hipEventCreateWithFlags(&h->gfork, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; ok && k < groups; ++k)
+        ok = hipStreamCreateWithFlags(&h->gstream[k], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&h->gjoin[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        (void)hip_status();
+        free_groups(h);
+        return SWARM_ERR_HIP;
+    }
+    h->groups = groups;
+    return SWARM_OK;
+}
+
 int32_t swarm_destroy(swarm_handle_t* h) {
     if (!h) return SWARM_ERR_ARG;
+    free_groups(h);
     if (h->d_mask) (void)hipFree(h->d_mask);
+    if (h->d_cost) (void)hipFree(h->d_cost);
     delete h;
     return SWARM_OK;
 }
@@ -232,10 +272,34 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     h->lens_exact = h->mirror.buckets.size() <= 1;
     if (h->lens_exact && !h->mirror.buckets.empty())
         h->lens.assign(h->p.num_envs, (int32_t)(h->mirror.buckets.begin()->first + h->mirror.offset));
-    const DevState st = dev_state(state);
+    const hipStream_t cs = (hipStream_t)stream;
+    if (!h->d_cost) {   // allocated once; written by kernels built with SWARM_PRED_PRIO
+        if (hipMalloc(&h->d_cost, (size_t)h->p.num_envs) != hipSuccess ||
+            hipMemsetAsync(h->d_cost, 0, (size_t)h->p.num_envs, cs) != hipSuccess)
+            return hip_status();
+    }
+    DevState st = dev_state(state);
+    st.cost = h->d_cost;
     const DevOut o{out->obs, out->reward, out->truncated};
-    launch_step(h->g, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any,
-                (hipStream_t)stream);
+    if (h->groups > 1 && h->g.layout == 103) {
+        // fork: every group stream waits for the caller's stream; join: the caller's
+        // stream waits for every group (one arena per workgroup, ranges of E / groups)
+        if (hipEventRecord(h->gfork, cs) != hipSuccess) return hip_status();
+        const int E = h->p.num_envs, K = h->groups;
+        for (int k = 0; k < K; ++k) {
+            Geom gk = h->g;
+            gk.env0 = (int32_t)((int64_t)E * k / K);
+            gk.env_n = (int32_t)((int64_t)E * (k + 1) / K) - gk.env0;
+            if (hipStreamWaitEvent(h->gstream[k], h->gfork, 0) != hipSuccess) return hip_status();
+            launch_step(gk, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any,
+                        h->gstream[k]);
+            if (hipEventRecord(h->gjoin[k], h->gstream[k]) != hipSuccess ||
+                hipStreamWaitEvent(cs, h->gjoin[k], 0) != hipSuccess)
+                return hip_status();
+        }
+    } else {
+        launch_step(h->g, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any, cs);
+    }
     h->tick += (uint64_t)n_substeps;
     return hip_status();
 }

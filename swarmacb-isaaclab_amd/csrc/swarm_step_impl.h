@@ -91,6 +91,23 @@
 #ifndef SWARM_PRIO_T
 #define SWARM_PRIO_T 2
 #endif
+// Predicted priority (layout 103): each launch stores its arena's count of moving
+// solver iterations (DevState::cost, a library-owned byte per env); the next launch
+// starts at s_setprio 1 / 2 / 3 if that count reached P1 / P2 / P3 (contact
+// clusters persist across decisions), instead of waiting for the graded bumps.
+// The bumps still raise it, never lower it. 0: off. Scheduling only.
+#ifndef SWARM_PRED_PRIO
+#define SWARM_PRED_PRIO 0
+#endif
+#ifndef SWARM_PRED_P1
+#define SWARM_PRED_P1 6
+#endif
+#ifndef SWARM_PRED_P2
+#define SWARM_PRED_P2 10
+#endif
+#ifndef SWARM_PRED_P3
+#define SWARM_PRED_P3 14
+#endif
 
 // 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
 // correction (bitwise = sqrtf); 0: the library's sqrtf.
@@ -131,9 +148,27 @@ namespace swarm {
 #include "swarm_geom_tables.inc"
 
 #if SWARM_WAVE_TIMING
-// per wave: {start clock lo, end - start, HW_ID, XCC_ID}, {wall start lo, wall end lo, solver passes, work}
+// per wave: {start clock lo, end - start, HW_ID, XCC_ID}, {wall start lo, wall end lo, solver passes, work},
+// {work counters}, then kWtPhases shader-clock sums of the phases below (4 uint4)
 constexpr int kWaveLogMax = 65536;
-static __device__ uint4 g_wave_log[3 * kWaveLogMax];
+constexpr int kWaveLogRow = 7;
+enum WtPhase : int {
+    PH_ACT_INT = 0,   // actions + integrate (+ the decimation sincos)
+    PH_SOLVE,         // env.step contact solver (all passes; includes the PH_PUSH_* below)
+    PH_RESOLVE,       // the all-env re-solve after a time-out (DG:1262)
+    PH_REWARD,        // dones, rewards, terminal critic, spawn
+    PH_PUBLISH,       // observation: position tile + inside flags + exchange point
+    PH_PROX,          // proximity partial (walls + robot discs)
+    PH_RAB,           // range-and-bearing partial (LOS, packet loss draws)
+    PH_COMBINE,       // partial-sum exchange of the 3 lanes of a robot
+    PH_FINISH,        // aggregates, light, ground, observation stores
+    PH_PUSH_PUB,      // push: position publish + exchange point
+    PH_PUSH_CAND,     // push: candidate mask of the lane's neighbour chunk
+    PH_PUSH_PAIRS,    // push: exact pair terms of the candidates
+    PH_PUSH_XCHG,     // push: partial-sum exchange and update
+    kWtPhases
+};
+static __device__ uint4 g_wave_log[kWaveLogRow * kWaveLogMax];
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m));
@@ -276,15 +311,24 @@ struct Lane {
     uint32_t seed_lo, seed_hi;
 #if SWARM_PRIO_MODE
     mutable int moved_iters;   // wave-uniform count of solver iterations that moved a robot
+    mutable int prio;          // wave-uniform current s_setprio level
 #endif
 #if SWARM_WAVE_TIMING
     mutable uint32_t wt_push, wt_pair, wt_rab, wt_seg, wt_disc;   // per-lane work counters (diagnostic)
+    mutable uint32_t wt_ph[kWtPhases];                            // shader clocks per phase (diagnostic)
 #endif
 };
 #if SWARM_WAVE_TIMING
 #define SWARM_WT(stmt) stmt
+// phase stamps: SWARM_PH_T(t) opens, SWARM_PH_ADD(L, k, t) charges the clocks since t to phase k
+#define SWARM_PH_T(t) uint64_t t = __builtin_amdgcn_s_memtime()
+#define SWARM_PH_ADD(L, k, t) ((L).wt_ph[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t)))
+#define SWARM_PH_NEXT(L, k, t) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); (L).wt_ph[k] += (uint32_t)(_n - (t)); t = _n; } while (0)
 #else
 #define SWARM_WT(stmt)
+#define SWARM_PH_T(t)
+#define SWARM_PH_ADD(L, k, t)
+#define SWARM_PH_NEXT(L, k, t)
 #endif
 
 // Philox counter (global env, robot | block << 8 | purpose << 24, tick), key = seed.
@@ -323,9 +367,9 @@ __device__ __forceinline__ void sync_wg() {
 // one more unit of wave-uniform work seen: raise the priority at T, 2T, 3T units
 __device__ __forceinline__ void prio_bump(const Lane& L) {
     const int c = ++L.moved_iters;
-    if (c == SWARM_PRIO_T) __builtin_amdgcn_s_setprio(1);
-    if (c == 2 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(2);
-    if (c == 3 * SWARM_PRIO_T) __builtin_amdgcn_s_setprio(3);
+    if (c == SWARM_PRIO_T && L.prio < 1) { __builtin_amdgcn_s_setprio(1); L.prio = 1; }
+    if (c == 2 * SWARM_PRIO_T && L.prio < 2) { __builtin_amdgcn_s_setprio(2); L.prio = 2; }
+    if (c == 3 * SWARM_PRIO_T && L.prio < 3) { __builtin_amdgcn_s_setprio(3); L.prio = 3; }
 }
 #endif
 
@@ -448,8 +492,10 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
                                             PairList* vl = nullptr) {
     if (SWARM_ABLATE & 4) return false;
     SWARM_WT(L.wt_push++);
+    SWARM_PH_T(wt_t);
     if (L.p == 0) S.xy[L.r] = make_float2(x, y);
     sync_wg<LY>();
+    SWARM_PH_NEXT(L, PH_PUSH_PUB, wt_t);
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
@@ -506,10 +552,12 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
                 return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
             });
         }
+        SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
             pair_term(j, x - p.x, y - p.y);
         });
+        SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -535,6 +583,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
             if (!__any(rx != 0.0f || ry != 0.0f || cx != 0.0f || cy != 0.0f)) {
                 x = (x + 0.0f) - 0.0f;
                 y = (y + 0.0f) - 0.0f;
+                SWARM_PH_ADD(L, PH_PUSH_XCHG, wt_t);
                 return false;
             }
         }
@@ -558,6 +607,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     }
     x = (x + rx) - cx;
     y = (y + ry) - cy;
+    SWARM_PH_ADD(L, PH_PUSH_XCHG, wt_t);
     return true;
 }
 
@@ -1325,7 +1375,9 @@ template <int MISSION, int PROFILE, int LY, int C>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw) {
+    SWARM_PH_T(wt_t);
     publish<LY>(g, L, S, x, y);
+    SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
     sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
 #pragma unroll
@@ -1340,9 +1392,12 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     } else {
         proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox);
     }
+    SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
         rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy);
+    SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
+    SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
     proximity_aggregate(g, prox, agg.pv, agg.pa);
     light<MISSION>(g, x, y, cyw, syw, lt, agg.lv, agg.la);
     rab_finish(g, n, wx, wy, zt, r4);
@@ -1372,6 +1427,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
             *reinterpret_cast<float4*>(o) = make_float4(gv, gv, gv, zt);
         }
     }
+    SWARM_PH_ADD(L, PH_FINISH, wt_t);
 }
 
 // standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
@@ -1540,9 +1596,12 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime k
     L.amask = m;
 #if SWARM_PRIO_MODE
     L.moved_iters = 0;
+    L.prio = 0;
 #endif
 #if SWARM_WAVE_TIMING
     L.wt_push = L.wt_pair = L.wt_rab = L.wt_seg = L.wt_disc = 0;
+#pragma unroll
+    for (int k = 0; k < kWtPhases; ++k) L.wt_ph[k] = 0;
 #endif
     return L;
 }
@@ -1562,6 +1621,16 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
     const Lane L = make_lane<NA, LY>(gr);
+#if SWARM_PRIO_MODE && SWARM_PRED_PRIO
+    if constexpr (LY == 103) {
+        if (st.cost) {   // one arena per wave: the byte is wave-uniform
+            const int pc = __builtin_amdgcn_readfirstlane((int)st.cost[L.valid ? L.env : 0]);
+            if (pc >= SWARM_PRED_P3) { __builtin_amdgcn_s_setprio(3); L.prio = 3; }
+            else if (pc >= SWARM_PRED_P2) { __builtin_amdgcn_s_setprio(2); L.prio = 2; }
+            else if (pc >= SWARM_PRED_P1) { __builtin_amdgcn_s_setprio(1); L.prio = 1; }
+        }
+    }
+#endif
     // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
     const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
     const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
@@ -1619,6 +1688,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, (size_t)EN, (size_t)q, tick};
 
         // ------------------------------ actions ------------------------------
+        SWARM_PH_T(wt_t);
         float lw, rw;
         if constexpr (PROFILE == STANDALONE) {
             const float* u_d = rp.rab_d ? rp.rab_d + ((size_t)s * L.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N
@@ -1656,7 +1726,9 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
                 const float qx = x, qy = y;
                 if (d > 0) sincosf(yaw, &syaw, &cyaw);
                 integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
+                SWARM_PH_NEXT(L, PH_ACT_INT, wt_t);
                 if (!(SWARM_ABLATE & 16)) solve<MISSION, LY, C, true>(g, L, S, x, y, qx, qy);
+                SWARM_PH_NEXT(L, PH_SOLVE, wt_t);
             }
             ep_len += 1;
             tout = ep_len >= gr.max_len;                                     // DG:1200-1209
@@ -1676,13 +1748,16 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
                 ep_rew = 0.0f;
                 if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
             }
+            SWARM_PH_NEXT(L, PH_REWARD, wt_t);
             if ((reset_any >> s) & 1ull)                                     // DG:1262 (all envs)
                 solve<MISSION, LY, C, false>(g, L, S, x, y, 0.0f, 0.0f);
+            SWARM_PH_NEXT(L, PH_RESOLVE, wt_t);
             if (tout) {
                 gprev = ground_code<MISSION, PROFILE>(g, x, y);
                 fsm = 0u;
                 if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
             }
+            SWARM_PH_ADD(L, PH_REWARD, wt_t);
         } else {
             integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
             walls_mc(g, x, y);
@@ -1731,6 +1806,9 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             st.comp_rew[L.env] = comp;
             if (out.reward) out.reward[L.env] = rew_acc;
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
+#if SWARM_PRIO_MODE && SWARM_PRED_PRIO
+            if (LY == 103 && st.cost) st.cost[L.env] = (uint8_t)min(L.moved_iters, 255);
+#endif
         }
     }
 #if SWARM_WAVE_TIMING
@@ -1742,9 +1820,15 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         const uint32_t push = wave_max(L.wt_push), pair = wave_max(L.wt_pair), rab = wave_max(L.wt_rab);
         const uint32_t seg = wave_max(L.wt_seg), disc = wave_max(L.wt_disc);
         if (threadIdx.x == 0 && blockIdx.x < kWaveLogMax) {
-            g_wave_log[3 * blockIdx.x] = make_uint4((uint32_t)wt_c0, (uint32_t)(wt_c1 - wt_c0), hw, xcc);
-            g_wave_log[3 * blockIdx.x + 1] = make_uint4((uint32_t)wt_w0, (uint32_t)wt_w1, push, pair);
-            g_wave_log[3 * blockIdx.x + 2] = make_uint4(rab, seg, disc, 0u);
+            uint4* row = g_wave_log + kWaveLogRow * blockIdx.x;
+            row[0] = make_uint4((uint32_t)wt_c0, (uint32_t)(wt_c1 - wt_c0), hw, xcc);
+            row[1] = make_uint4((uint32_t)wt_w0, (uint32_t)wt_w1, push, pair);
+            row[2] = make_uint4(rab, seg, disc, 0u);
+            uint32_t ph[16] = {};
+#pragma unroll
+            for (int k = 0; k < kWtPhases; ++k) ph[k] = L.wt_ph[k];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) row[3 + k] = make_uint4(ph[4 * k], ph[4 * k + 1], ph[4 * k + 2], ph[4 * k + 3]);
         }
     }
 #endif

@@ -222,3 +222,37 @@ def test_partial_resets_then_timeouts(gpu_device):
         assert bool(eng.last_timeouts & 1) == expect
         np.testing.assert_array_equal(tr.cpu().numpy().astype(bool), lens_before + 1 >= max_len)
     eng.close()
+
+
+@pytest.mark.parametrize("mission,discrete,obs_dim", [("homing", False, 24), ("foraging", True, 4)])
+def test_step_groups_bitwise(mission, discrete, obs_dim, gpu_device):
+    """swarm_set_step_groups: a step split into 2, 3 or 8 env ranges on the handle's own
+    streams gives bit for bit the single launch's state and outputs (uneven ranges,
+    staggered time-outs, fused 5-step decisions)."""
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    E, seed = 1000, 777
+    rng = np.random.default_rng(5)
+    acts = [rng.integers(0, 6, (E, 20)).astype(np.int32) if discrete
+            else (np.clip(rng.normal(size=(E, 20, 2)), -3, 3) / 3).astype(np.float32) for _ in range(12)]
+    runs = []
+    for groups in (1, 2, 3, 8):
+        eng = SwarmEngine(mission, "isaac", E, 20, obs_dim, discrete, 1800, 1, 0, seed, gpu_device,
+                          step_groups=groups)
+        eng.reset()
+        _stagger_timeouts(eng, [(np.arange(3, 13), 3), (np.arange(400, 407), 17), ([E - 1], 31)])
+        outs = []
+        for k in range(12):
+            obs, rew, tr = eng.step(torch.as_tensor(acts[k]).to(gpu_device), 5)
+            outs.append((obs.clone(), rew.clone(), tr.clone()))
+        torch.cuda.synchronize(gpu_device)
+        runs.append((eng.dump_state(), [tuple(t.cpu().numpy() for t in o) for o in outs]))
+        eng.close()
+    ref_state, ref_outs = runs[0]
+    assert sum(int(o[2].sum()) for o in ref_outs) >= 18
+    for groups, (st, outs) in zip((2, 3, 8), runs[1:]):
+        for key in ref_state:
+            assert np.array_equal(ref_state[key], st[key]), f"groups={groups}: state {key} differs"
+        for k, (a, b) in enumerate(zip(ref_outs, outs)):
+            for name, x, y in zip(("obs", "reward", "trunc"), a, b):
+                assert np.array_equal(x, y), f"groups={groups}: decision {k} {name} differs"

@@ -4,7 +4,7 @@
 #   tools/variants.sh run                                         (GPU box: bench each lib x WAVES)
 set -o pipefail
 cd "$(dirname "$0")/.."
-OUT=build/variants
+OUT=${VOUT:-build/variants}
 if [ "$1" = build ]; then
   make -s -j8 -C swarmacb-isaaclab_amd/csrc || exit 1
   rm -rf $OUT && mkdir -p $OUT

@@ -24,6 +24,10 @@ sys.path.insert(0, os.path.join(ROOT, "swarmacb-isaaclab_amd"))
 from SwarmACB_isaac.engine import SwarmEngine  # noqa: E402
 
 
+PHASES = ["act_int", "solve", "resolve", "reward", "publish", "prox", "rab", "combine", "finish",
+          "push_pub", "push_cand", "push_pairs", "push_xchg"]   # swarm_step_impl.h WtPhase
+
+
 def pct(a, qs=(0, 10, 50, 90, 99, 100)):
     return {f"p{q}": float(np.percentile(a, q)) for q in qs}
 
@@ -48,7 +52,7 @@ def main():
     for d in range(300):
         eng.step(acts[d], dp, out=out)
     torch.cuda.synchronize(dev)
-    buf = np.zeros((E, 3, 4), np.uint32)
+    buf = np.zeros((E, 7, 4), np.uint32)
     rows = []
     for d in range(300, 310):
         st = eng.dump_state()
@@ -91,6 +95,17 @@ def main():
             v = v.astype(np.float64)
             rows[-1][f"{k}_mean_all_vs_slowest1pct"] = [float(v.mean()), float(v[slow].mean())]
             rows[-1][f"corr_life_{k}"] = float(np.corrcoef(life_ns, v)[0, 1]) if v.std() > 0 else None
+        # shader clocks per phase (the push phases are inside "solve"/"resolve"), as a
+        # fraction of the wave's life; mean over all waves and over the slowest 1 %
+        ph = buf[:, 3:7, :].reshape(E, 16)[:, :len(PHASES)].astype(np.float64)
+        lf = np.maximum(life.astype(np.float64), 1.0)
+        rows[-1]["phase_frac_mean"] = {k: float((ph[:, i] / lf).mean()) for i, k in enumerate(PHASES)}
+        rows[-1]["phase_frac_slowest1pct"] = {k: float((ph[slow, i] / lf[slow]).mean()) for i, k in enumerate(PHASES)}
+        rows[-1]["phase_kclk_mean"] = {k: float(ph[:, i].mean() / 1e3) for i, k in enumerate(PHASES)}
+        rows[-1]["life_kclk_mean"] = float(life.mean() / 1e3)
+        pushes = np.maximum(buf[:, 1, 2].astype(np.float64), 1.0)
+        rows[-1]["clk_per_push"] = {k: float((ph[:, PHASES.index(k)] / pushes).mean())
+                                    for k in ("push_pub", "push_cand", "push_pairs", "push_xchg")}
         A = np.stack([np.ones(E)] + [w.astype(np.float64) for w in work.values()], 1)
         coef, *_ = np.linalg.lstsq(A, life_ns / 1e3, rcond=None)
         pred = A @ coef
