@@ -4,6 +4,7 @@ one library GEMM vs the row-chunked batched GEMM + chunk sum of
 poca_networks._SplitKLinear, per chunk size. Event-timed on the current stream."""
 
 import json
+import os
 
 import torch
 
@@ -50,5 +51,26 @@ def main():
             out.append(row)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("GEMM_BIAS"):
     main()
+
+
+def bias_grads():
+    """db = column sums of dy over R rows: the chunked reduction _SplitKLinear uses vs
+    alternatives."""
+    dev = torch.device("cuda")
+    for R, M in ((40960, 384), (81920, 384), (81920, 128), (122880, 128)):
+        dy = torch.randn(R, M, device=dev)
+        L = 1024
+        c = R // L
+        ones = torch.ones(c, 1, L, device=dev)
+        row = {"R": R, "M": M,
+               "chunked_us": timed(lambda: dy.view(c, L, M).sum(dim=1).sum(dim=0)),
+               "plain_us": timed(lambda: dy.sum(dim=0)),
+               "bmm_ones_us": timed(lambda: torch.bmm(ones, dy.view(c, L, M)).sum(dim=0)),
+               "mv_us": timed(lambda: dy.t().mv(torch.ones(R, device=dev)))}
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__" and os.environ.get("GEMM_BIAS"):
+    bias_grads()
