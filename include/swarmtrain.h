@@ -69,6 +69,15 @@ int32_t swarm_rsa_attn_forward(int64_t S, int32_t N, int32_t H, int32_t D, const
 int32_t swarm_rsa_attn_backward(int64_t S, int32_t N, int32_t H, int32_t D, const float* qkv, const float* key_mask,
                                 const float* d_att, float* d_qkv, void* stream);
 
+/* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
+ * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
+ * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.
+ * Replaces the per-tensor clone / where / copy_ of the OC2 update's KL rollback
+ * (learned_option_critic_trainer.py:1421-1660: an actor step the early stop rejects leaves the
+ * parameters and Adam state as they were) with one launch per direction. */
+int32_t swarm_tensor_list_copy(int32_t n, const uint64_t* dst_ptrs, const uint64_t* src_ptrs, const int64_t* words,
+                               int64_t max_words, const uint8_t* unless, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -70,7 +70,7 @@ class GatherField(C.Structure):
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
 CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
-                 "swarm_rsa_attn_backward"]
+                 "swarm_rsa_attn_backward", "swarm_tensor_list_copy"]
 ATTN_MAX_ENTITIES = 32
 ATTN_HEAD_DIMS = (32, 64, 128)
 LSTM_SEQ_MAX_UNITS = 64
@@ -156,6 +156,8 @@ def load() -> C.CDLL:
     lib.swarm_rsa_attn_forward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp]
     lib.swarm_rsa_attn_backward.restype = i32
     lib.swarm_rsa_attn_backward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp, vp]
+    lib.swarm_tensor_list_copy.restype = i32
+    lib.swarm_tensor_list_copy.argtypes = [i32, vp, vp, vp, C.c_int64, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -28,6 +28,7 @@ decision identical; agents/distributed.py).
 from __future__ import annotations
 
 import copy
+import ctypes as C
 import time
 
 import torch
@@ -35,6 +36,7 @@ import torch.nn.functional as F
 import torch.optim as optim
 from torch.distributions import Bernoulli
 
+from .. import _native
 from ._trainer import PolynomialDecay, TrainerBase, stack_obs, trust_region_value_loss
 from .config import PAPER_PARITY_VERSION, LearnedOptionCriticConfig
 from .distributed import TrainerComm
@@ -508,6 +510,36 @@ class LearnedOptionCriticTrainer(TrainerBase):
             out += [p, st[p]["step"], st[p]["exp_avg"], st[p]["exp_avg_sq"]]
         return out
 
+    def _rollback_tables(self):
+        """Device pointer tables for swarm_tensor_list_copy over the actor's parameters and
+        Adam state (live) and a same-shaped save area, rebuilt when a tensor moved (a loaded
+        optimizer state). Built outside any capture: the graph replays the tables' contents."""
+        live = self._actor_step_tensors()
+        key = tuple(t.data_ptr() for t in live)
+        rb = getattr(self, "_rb", None)
+        if rb is None or rb["key"] != key:
+            for t in live:
+                if t.element_size() != 4 or not t.is_contiguous():
+                    raise RuntimeError("actor step tensors must be contiguous 32-bit tensors")
+            saved = [torch.empty_like(t) for t in live]
+            dev = live[0].device
+            i64 = dict(dtype=torch.int64, device=dev)
+            rb = {"key": key, "saved": saved, "n": len(live),
+                  "live_ptrs": torch.tensor([t.data_ptr() for t in live], **i64),
+                  "saved_ptrs": torch.tensor([t.data_ptr() for t in saved], **i64),
+                  "words": torch.tensor([t.numel() for t in live], **i64),
+                  "max_words": max(t.numel() for t in live)}
+            self._rb = rb
+        return rb
+
+    def _list_copy(self, dst_ptrs, src_ptrs, unless=None):
+        rb = self._rb
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(dst_ptrs.device).cuda_stream)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
+        _native.check(lib.swarm_tensor_list_copy(rb["n"], ptr(dst_ptrs), ptr(src_ptrs), ptr(rb["words"]),
+                                                 rb["max_words"], ptr(unless), stream), "swarm_tensor_list_copy")
+
     def _clip_step_device(self, loss, comm, optimizer, params, max_norm: float):
         """_clip_step without host synchronisation (finiteness is checked after the update)."""
         comm.zero_grad(optimizer)
@@ -535,12 +567,22 @@ class LearnedOptionCriticTrainer(TrainerBase):
         G["stopped"] |= over
         G["bad"][0] |= ~torch.isfinite(actor_loss.detach())
         G["bad"][1] |= ~torch.isfinite(critic_loss.detach())
-        saved = [t.detach().clone() for t in self._actor_step_tensors()]
-        norm_a = self._clip_step_device(actor_loss, self.actor_comm, self.actor_optimizer, self.actor_parameters,
-                                        cfg.actor_max_grad_norm)
-        with torch.no_grad():
-            for t, b in zip(self._actor_step_tensors(), saved):
-                t.copy_(torch.where(apply, t, b))
+        if self.device.type == "cuda":
+            # save the actor's parameters + Adam state, take the step, and copy the saved
+            # words back unless `apply` (one multi-tensor launch each way)
+            rb = self._rollback_tables()
+            self._list_copy(rb["saved_ptrs"], rb["live_ptrs"])
+            norm_a = self._clip_step_device(actor_loss, self.actor_comm, self.actor_optimizer, self.actor_parameters,
+                                            cfg.actor_max_grad_norm)
+            G["apply_u8"].copy_(apply)
+            self._list_copy(rb["live_ptrs"], rb["saved_ptrs"], unless=G["apply_u8"])
+        else:
+            saved = [t.detach().clone() for t in self._actor_step_tensors()]
+            norm_a = self._clip_step_device(actor_loss, self.actor_comm, self.actor_optimizer, self.actor_parameters,
+                                            cfg.actor_max_grad_norm)
+            with torch.no_grad():
+                for t, b in zip(self._actor_step_tensors(), saved):
+                    t.copy_(torch.where(apply, t, b))
         G["grad_norms"][0] += torch.where(apply, norm_a.double(), torch.zeros_like(G["grad_norms"][0]))
         G["bad"][2] |= apply & ~torch.isfinite(norm_a)
         G["actor_updates"] += apply.double()
@@ -565,11 +607,14 @@ class LearnedOptionCriticTrainer(TrainerBase):
                        "nb": torch.zeros((), **f64), "actor_updates": torch.zeros((), **f64),
                        "init_kl": torch.zeros((), **f64), "max_kl": torch.zeros(3, **f64),
                        "stopped": torch.zeros((), dtype=torch.bool, device=dev),
-                       "bad": torch.zeros(4, dtype=torch.bool, device=dev)}
+                       "bad": torch.zeros(4, dtype=torch.bool, device=dev),
+                       "apply_u8": torch.zeros((), dtype=torch.uint8, device=dev)}
         for t in self._g.values():
             t.zero_()
         self._init_adam_state(self.actor_optimizer)
         self._init_adam_state(self.critic_optimizer)
+        if dev.type == "cuda":
+            self._rollback_tables()
         step = self._step_runner(self._oc2_step, [self.actor_optimizer, self.critic_optimizer])
         key = (self.current_eps, self.current_beta, self.current_lr, self.current_actor_lr,
                self.current_termination_prior_coef, self.current_option_balance_coef)

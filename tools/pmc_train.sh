@@ -18,4 +18,7 @@ run_pass() {
 run_pass mfma SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_train/trace -o run --output-format csv \
   -- python3 tools/prof_train.py --config $CFG --steps 4 > gpurun_out/pmc_train/trace.log 2>&1 || { echo "trace failed"; exit 4; }
+# summarise on the box, then drop the raw per-dispatch files (the merge-back is capped at 64 MiB)
+python3 tools/pmc_train_table.py gpurun_out/pmc_train gpurun_out/pmc_train/mfma_table.csv > gpurun_out/pmc_train/mfma_table.txt || exit 5
+rm -f gpurun_out/pmc_train/mfma/run_counter_collection.csv gpurun_out/pmc_train/trace/run_kernel_trace.csv
 echo PMC_TRAIN_DONE
