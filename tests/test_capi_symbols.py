@@ -71,6 +71,28 @@ def test_create_destroy_and_call_order():
     assert lib.swarm_destroy(h) == 0
 
 
+def test_step_groups_argument_checks():
+    """swarm_set_step_groups validates before touching the device (1 = no streams)."""
+    lib = _native.load()
+    h = C.c_void_p()
+    assert lib.swarm_create(C.byref(_params(num_envs=4)), C.byref(h)) == 0
+    try:
+        assert lib.swarm_set_step_groups(h, 0) == -1
+        assert lib.swarm_set_step_groups(h, 9) == -1
+        assert lib.swarm_set_step_groups(h, 5) == -1      # more groups than envs
+        assert lib.swarm_set_step_groups(h, 1) == 0
+        assert lib.swarm_set_step_groups(None, 1) == -1
+    finally:
+        assert lib.swarm_destroy(h) == 0
+
+
+def test_tensor_list_copy_argument_checks():
+    lib = _native.load()
+    assert lib.swarm_tensor_list_copy(-1, None, None, None, 0, None, None) == -1
+    assert lib.swarm_tensor_list_copy(0, None, None, None, 0, None, None) == 0
+    assert lib.swarm_tensor_list_copy(2, None, None, None, 16, None, None) == -1
+
+
 def test_fsm_pack_matches_c_abi():
     lib = _native.load()
     rng = np.random.default_rng(0)
