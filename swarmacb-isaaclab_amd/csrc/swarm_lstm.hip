@@ -3,8 +3,9 @@
 //
 // One 256-thread workgroup per sequence walks all T steps: the forward keeps
 // its gate row of W_hh in registers (thread j = gate pre-activation j, up to
-// 4 x 64 units) and the carried (masked) h in LDS, so a step is one register dot
-// product, one activation, one cell update and two barriers; the backward keeps
+// 4 x 64 units) and the carried (masked) h in lane u of every wave, so a step is
+// U scalar broadcasts, one register dot product, one activation, one barrier and
+// one cell update; the backward keeps
 // the W_hh^T slice it needs in registers and walks the steps in reverse. A
 // minibatch of the ML-Agents trainers (16 sequences x 128 steps) is then one
 // launch instead of 128 library LSTM calls (forward) plus 128 (backward).
@@ -43,41 +44,39 @@ __device__ __forceinline__ float fast_sigmoid(float x) {
 }
 __device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigmoid(2.0f * x) - 1.0f; }
 
-// Forward: NF = 512 threads = 8 waves per sequence. Gate row j = t >> 1 is split over two
-// adjacent lanes (each a half of the U-long dot product with h, one DPP add joins them), so
-// a step's products are 2 waves per SIMD deep instead of one 64-long chain per lane. The
-// gates of a step go through ONE LDS buffer (double-buffered by step parity) and ONE
-// barrier; then every wave computes all U cell updates itself (lane u = unit u) and keeps
-// h in its own LDS row, so the next step's products need no second barrier.
-constexpr int NF = 512;
+// lane k's value of v, in a scalar register (v_readlane_b32 on the bit pattern)
+__device__ __forceinline__ float lane_bcast(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
 
+// Forward: NT = 256 threads = 4 waves per sequence, thread j = gate row j. Every wave
+// computes all U cell updates itself (lane u = unit u), so h_u sits in lane u of EVERY
+// wave and a gate row's product with h reads it by v_readlane into scalar registers:
+// no LDS round trip for h. The gates of a step go through one LDS buffer (double-buffered
+// by step parity) and ONE barrier. Per step: U readlanes + U FMAs (4 chains) per lane,
+// one activation, one LDS write / barrier / read, one cell update.
 template <int UC, bool KEEP>
-__global__ void __launch_bounds__(NF) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
+__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
                                                           const float* __restrict__ w_hh,
                                                           const float* __restrict__ h0,
                                                           const float* __restrict__ c0,
                                                           const float* __restrict__ keep, float* __restrict__ h_out,
                                                           float* __restrict__ c_out, float* __restrict__ act) {
     constexpr int KU = UC > 0 ? UC : MAXU;              // register extent of a gate row
-    constexpr int KH = (KU + 1) / 2;                     // per half-lane
     const int U = UC > 0 ? UC : U_rt;
-    const int UH = (U + 1) / 2;
-    __shared__ __attribute__((aligned(16))) float hs[NF / 64][MAXU];   // per-wave copy of h
     __shared__ __attribute__((aligned(16))) float gs[2][4 * MAXU];
     const int64_t b = blockIdx.x;
-    const int t_id = threadIdx.x;
-    const int wave = t_id >> 6, lane = t_id & 63;
+    const int j = threadIdx.x;
+    const int wave = j >> 6, lane = j & 63;
     const int G = 4 * U;
-    const int j = t_id >> 1, half = t_id & 1;
     const bool row_j = j < G;
     const int jc = row_j ? j : G - 1;
-    const int k0 = half * UH;                            // this lane's half of the dot product
-    float w[KH];
+    float w[KU];
 #pragma unroll
-    for (int k = 0; k < KH; ++k) w[k] = (row_j && k < UH && k0 + k < U) ? w_hh[jc * U + k0 + k] : 0.0f;
+    for (int k = 0; k < KU; ++k) w[k] = (row_j && k < U) ? w_hh[jc * U + k] : 0.0f;
     const bool unit = lane < U;                          // lane u = unit u in every wave
     float c = unit ? c0[b * U + lane] : 0.0f;
-    hs[wave][lane] = unit ? h0[b * U + lane] : 0.0f;
+    float h = unit ? h0[b * U + lane] : 0.0f;            // 0 in lanes >= U (their w columns are 0 too)
     const int kind = jc / U;                             // 0 i, 1 f, 2 g, 3 o
     const float* xb = xg + b * T * G + jc;
     auto load_group = [&](int t0, float* xr, float* kr) {
@@ -90,8 +89,6 @@ __global__ void __launch_bounds__(NF) lstm_seq_fwd_kernel(int T, int U_rt, const
     };
     float xr[PF], kr[PF] = {};
     load_group(0, xr, kr);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     for (int t0 = 0; t0 < T; t0 += PF) {
         float xn[PF], kn[PF] = {};
         load_group(t0 + PF, xn, kn);
@@ -101,48 +98,39 @@ __global__ void __launch_bounds__(NF) lstm_seq_fwd_kernel(int T, int U_rt, const
             if (t >= T) break;
             const int64_t row = b * T + t;
             float* g = gs[t & 1];
-            {
-                const float* h = &hs[wave][k0];
-                float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-                if constexpr (UC > 0 && KH % 4 == 0) {
+            // all U broadcasts first (scalar registers), then the products: a readlane's
+            // result read by the very next VALU instruction costs wait states
+            float hk[KU];
 #pragma unroll
-                    for (int k = 0; k < KH; k += 4) {
-                        const float4 h4 = *reinterpret_cast<const float4*>(h + k);
-                        a0 += w[k] * h4.x;
-                        a1 += w[k + 1] * h4.y;
-                        a2 += w[k + 2] * h4.z;
-                        a3 += w[k + 3] * h4.w;
-                    }
-                } else {
+            for (int k = 0; k < KU; ++k) hk[k] = lane_bcast(h, k);
+            __builtin_amdgcn_sched_barrier(0);
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
 #pragma unroll
-                    for (int k = 0; k < KH; ++k)
-                        if (k < UH) a0 += w[k] * h[k];
-                }
-                float a = (a0 + a1) + (a2 + a3);
-                a += __shfl_xor(a, 1);                   // the other half of row j
-                if (row_j && half == 0) {
-                    a += xr[p];
-                    const float v = kind == 2 ? fast_tanh(a) : fast_sigmoid(a);
-                    g[j] = v;
-                    act[row * G + j] = v;
-                }
+            for (int k = 0; k < KU; k += 4) {
+                a0 = fmaf(w[k], hk[k], a0);
+                if (k + 1 < KU) a1 = fmaf(w[k + 1], hk[k + 1], a1);
+                if (k + 2 < KU) a2 = fmaf(w[k + 2], hk[k + 2], a2);
+                if (k + 3 < KU) a3 = fmaf(w[k + 3], hk[k + 3], a3);
+            }
+            const float a = ((a0 + a1) + (a2 + a3)) + xr[p];
+            const float v = kind == 2 ? fast_tanh(a) : fast_sigmoid(a);
+            if (row_j) {
+                g[j] = v;
+                act[row * G + j] = v;
             }
             __syncthreads();
             if (unit) {
                 c = g[U + lane] * c + g[lane] * g[2 * U + lane];
-                const float h = g[3 * U + lane] * fast_tanh(c);
+                h = g[3 * U + lane] * fast_tanh(c);
                 if (wave == 0) {
                     h_out[row * U + lane] = h;
                     c_out[row * U + lane] = c;
                 }
                 // the state carried into step t + 1 is masked where the episode ended at t
                 const float kk = (KEEP && t + 1 < T) ? kr[p] : 1.0f;
-                hs[wave][lane] = h * kk;
+                h *= kk;
                 c *= kk;
             }
-            // h is read back by this wave only: wave-scope ordering, no barrier
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            __builtin_amdgcn_wave_barrier();
         }
 #pragma unroll
         for (int p = 0; p < PF; ++p) {
@@ -273,7 +261,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
 template <int UC, bool KEEP>
 void launch_fwd(int64_t n, int T, int U, const float* xg, const float* w_hh, const float* h0, const float* c0,
                 const float* keep, float* h_out, float* c_out, float* act, hipStream_t st) {
-    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NF, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
+    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
 }
 
 template <int UC, bool KEEP>
