@@ -56,6 +56,42 @@ int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float
                                 const float* dh_n, const float* dc_n, float* dxg, float* dh0, float* dc0,
                                 void* stream);
 
+/* Several independent recurrences (same T and units, e.g. the actor's and the critic's memories
+ * of one minibatch, or the three OC2 critics) in ONE launch: problem k's sequences are workgroups
+ * [first_k, first_k + n_k) of one grid, so the launches' latency chains overlap instead of running
+ * back to back. Fields as in swarm_lstm_seq_forward / _backward; keep may be NULL per problem;
+ * 1 <= count <= SWARM_LSTM_MAX_BATCH. The single-problem calls above are count = 1 of these. */
+#define SWARM_LSTM_MAX_BATCH 6
+typedef struct {
+    int64_t n;
+    const float* xg;
+    const float* w_hh;
+    const float* h0;
+    const float* c0;
+    const float* keep;
+    float* h_out;
+    float* c_out;
+    float* act;
+} swarm_lstm_seq_fwd_t;
+typedef struct {
+    int64_t n;
+    const float* w_hh;
+    const float* c0;
+    const float* keep;
+    const float* c_out;
+    const float* act;
+    const float* dh_out;
+    const float* dh_n;
+    const float* dc_n;
+    float* dxg;
+    float* dh0;
+    float* dc0;
+} swarm_lstm_seq_bwd_t;
+int32_t swarm_lstm_seq_forward_batch(int32_t count, int32_t T, int32_t units, const swarm_lstm_seq_fwd_t* seqs,
+                                     void* stream);
+int32_t swarm_lstm_seq_backward_batch(int32_t count, int32_t T, int32_t units, const swarm_lstm_seq_bwd_t* seqs,
+                                      void* stream);
+
 /* Training-time attention core of ResidualSelfAttention (reference agents/poca_networks.py:417-491,
  * replaces the autograd bmm / softmax / bmm path of every PPO optimizer step): per entity set s
  * (S sets of N <= 32 entities) and head h (H heads of d = D / H in {32, 64, 128} columns),

@@ -70,7 +70,19 @@ class GatherField(C.Structure):
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
 CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
-                 "swarm_rsa_attn_backward", "swarm_tensor_list_copy"]
+                 "swarm_rsa_attn_backward", "swarm_tensor_list_copy", "swarm_lstm_seq_forward_batch",
+                 "swarm_lstm_seq_backward_batch"]
+LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
+
+
+class LstmSeqFwd(C.Structure):
+    _fields_ = [("n", C.c_int64)] + [(f, C.c_void_p) for f in ("xg", "w_hh", "h0", "c0", "keep", "h_out", "c_out",
+                                                                  "act")]
+
+
+class LstmSeqBwd(C.Structure):
+    _fields_ = [("n", C.c_int64)] + [(f, C.c_void_p) for f in ("w_hh", "c0", "keep", "c_out", "act", "dh_out", "dh_n",
+                                                                  "dc_n", "dxg", "dh0", "dc0")]
 ATTN_MAX_ENTITIES = 32
 ATTN_HEAD_DIMS = (32, 64, 128)
 LSTM_SEQ_MAX_UNITS = 64
@@ -152,6 +164,10 @@ def load() -> C.CDLL:
     lib.swarm_lstm_seq_forward.argtypes = [C.c_int64, i32, i32] + [vp] * 9
     lib.swarm_lstm_seq_backward.restype = i32
     lib.swarm_lstm_seq_backward.argtypes = [C.c_int64, i32, i32] + [vp] * 12
+    lib.swarm_lstm_seq_forward_batch.restype = i32
+    lib.swarm_lstm_seq_forward_batch.argtypes = [i32, i32, i32, vp, vp]
+    lib.swarm_lstm_seq_backward_batch.restype = i32
+    lib.swarm_lstm_seq_backward_batch.argtypes = [i32, i32, i32, vp, vp]
     lib.swarm_rsa_attn_forward.restype = i32
     lib.swarm_rsa_attn_forward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp]
     lib.swarm_rsa_attn_backward.restype = i32

@@ -44,7 +44,7 @@ from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
 from .learned_option_critic_networks import (LEARNED_OPTION_CRITIC_VERSION, LearnedOptionActor,
                                              termination_objective)
 from .option_collector import LearnedOptionCollector
-from .poca_networks import POCACritic
+from .poca_networks import POCACritic, batched_sequence_passes
 
 __all__ = ["LearnedOptionCriticConfig", "LearnedOptionCriticTrainer", "stable_trust_region_policy_loss"]
 
@@ -381,15 +381,15 @@ class LearnedOptionCriticTrainer(TrainerBase):
         def mem(k):
             return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
 
-        new_team = self.team_critic.critic_pass(flat_states, mem("team_memory"), sequence_length=L).squeeze(-1)
-        new_action_bl = self.action_critic.focal_baselines(option_states, flat_joint_actions, focal_ids,
-                                                           mem("action_baseline_memory"),
-                                                           sequence_length=L).squeeze(-1)
-        # the option critic's joint_action_pass and focal_baselines as one batched pass
-        new_joint, new_option_bl = self.option_critic.sequence_passes(
-            flat_states, encoded, focal_ids,
-            {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")},
-            sequence_length=L, passes=("joint", "baseline"))
+        # team critic_pass, action-critic focal_baselines and the option critic's joint_action_pass +
+        # focal_baselines (one batched pass): the three critics' memories in ONE LSTM launch
+        ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes([
+            (self.team_critic, flat_states, None, focal_ids, {"value": mem("team_memory")}, L, ("value",)),
+            (self.action_critic, option_states, flat_joint_actions, focal_ids,
+             {"baseline": mem("action_baseline_memory")}, L, ("baseline",)),
+            (self.option_critic, flat_states, encoded, focal_ids,
+             {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")}, L,
+             ("joint", "baseline"))])
 
         def tr_loss(new, old_key):
             return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,

@@ -42,11 +42,15 @@ class FixedOptionManager(nn.Module):
     def forward_sequence(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
         """(B, T, obs) -> selector logits (B, T, O), termination logits (B, T, O), memory.
         keep (B, T): the memory is multiplied by keep[:, t] after step t."""
+        out, nxt = _lstm(*self.sequence_lstm_item(obs_seq, state, keep))
+        return self.option_head(out), self.termination_head(out), nxt
+
+    def sequence_lstm_item(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
+        """forward_sequence up to its LSTM: (lstm, encoded sequence, state, keep) for
+        poca_networks.lstm_sequences; the heads then take the LSTM output."""
         B, T = obs_seq.shape[:2]
         enc = self.encoder(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
-        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device),
-                         keep)
-        return self.option_head(out), self.termination_head(out), nxt
+        return self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device), keep
 
     def step(self, obs: torch.Tensor, state=None):
         opt, term, nxt = self.forward_sequence(obs.unsqueeze(1), state)

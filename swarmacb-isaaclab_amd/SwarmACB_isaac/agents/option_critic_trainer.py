@@ -32,7 +32,7 @@ from .config import PAPER_PARITY_VERSION, FixedOptionCriticConfig
 from .option_collector import FixedOptionCollector
 from .option_critic_buffer import FixedOptionRolloutBuffer
 from .option_critic_networks import FixedOptionManager
-from .poca_networks import POCACritic
+from .poca_networks import POCACritic, lstm_sequences
 
 __all__ = ["FixedOptionCriticConfig", "FixedOptionCriticTrainer", "OPTION_CRITIC_VERSION"]
 
@@ -112,13 +112,17 @@ class FixedOptionCriticTrainer(TrainerBase):
         self.collector.reset_state()
 
     # ------------------------------------------------------------ losses
-    def _manager_sequence(self, batch: dict):
+    def _manager_sequence(self, batch: dict, other_item=None):
         """Selector logits of the manager over the minibatch sequences with the memory of
         rows whose episode ended at t zeroed before step t+1 (the per-step loop of
-        OCT:492-509, as one masked sequence)."""
+        OCT:492-509, as one masked sequence). `other_item`: an independent LSTM item (the
+        critic's) run in the same launch (lstm_sequences); its output is returned too."""
         state = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
-        option_logits, _term, _ = self.manager.forward_sequence(batch["obs"], state, keep=1.0 - batch["dones"])
-        return option_logits
+        items = [self.manager.sequence_lstm_item(batch["obs"], state, keep=1.0 - batch["dones"])]
+        if other_item is not None:
+            items.append(other_item)
+        outs = lstm_sequences(items)
+        return self.manager.option_head(outs[0][0]), (outs[1][0] if other_item is not None else None)
 
     def _compute_sequence_losses(self, batch: dict, current_eps: float):
         """option_critic_trainer.py:459-666: (policy, value, joint option value, baseline,
@@ -130,7 +134,21 @@ class FixedOptionCriticTrainer(TrainerBase):
         B, L = batch["obs"].shape[:2]
         N = critic_states.shape[2]
 
-        option_logits = self._manager_sequence(batch)
+        def mem(k):
+            return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
+
+        flat_states = critic_states.reshape(B * L, N, -1)
+        flat_option_ids = batch["critic_options"].reshape(B * L, N)
+        critic_options = self._encode_options_for_critic(flat_option_ids)
+        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
+        # critic_pass, joint_action_pass and focal_baselines (OCT:571-608) as one batched pass
+        # (POCACritic.sequence_passes) whose memory shares the manager's LSTM launch
+        c_item, c_ctx = self.critic.sequence_passes_begin(
+            flat_states, critic_options, focal_ids,
+            {"value": mem("value_memory"), "joint": mem("joint_memory"), "baseline": mem("baseline_memory")},
+            sequence_length=L, passes=("value", "joint", "baseline"))
+        option_logits, c_out = self._manager_sequence(batch, c_item)
+        new_team_values, new_joint, new_baselines = self.critic.sequence_passes_end(c_out, c_ctx)
         opt_dist = Categorical(validate_args=False, logits=option_logits.reshape(B * L, O))
         new_logp = opt_dist.log_prob(options.reshape(-1)).view(B, L)
         ent = opt_dist.entropy().view(B, L)
@@ -158,23 +176,9 @@ class FixedOptionCriticTrainer(TrainerBase):
         next_beta_logits = next_term_logits.view(B, L, O).gather(-1, options.unsqueeze(-1)).squeeze(-1)
         next_beta = torch.sigmoid(next_beta_logits)
 
-        flat_states = critic_states.reshape(B * L, N, -1)
         flat_next_states = next_critic_states.reshape(B * L, N, -1)
-        flat_option_ids = batch["critic_options"].reshape(B * L, N)
-        critic_options = self._encode_options_for_critic(flat_option_ids)
         flat_returns = batch["returns"].reshape(B * L)
         flat_loss_mask = loss_mask.reshape(B * L)
-
-        def mem(k):
-            return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
-
-        # critic_pass, joint_action_pass and focal_baselines (OCT:571-608) as one batched pass
-        # (POCACritic.sequence_passes)
-        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        new_team_values, new_joint, new_baselines = self.critic.sequence_passes(
-            flat_states, critic_options, focal_ids,
-            {"value": mem("value_memory"), "joint": mem("joint_memory"), "baseline": mem("baseline_memory")},
-            sequence_length=L, passes=("value", "joint", "baseline"))
         value_loss = trust_region_value_loss(new_team_values, batch["old_team_values"].reshape(B * L), flat_returns,
                                              current_eps, flat_loss_mask, denom=d_mask)
         joint_loss = trust_region_value_loss(new_joint, batch["old_joint_option_values"].reshape(B * L),

@@ -131,47 +131,78 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
 
 
-class _LSTMSequence(torch.autograd.Function):
-    """Whole-sequence LSTM recurrence on swarm_lstm_seq_forward / _backward
-    (include/swarmtrain.h): inputs are the gate pre-activations xg = x W_ih^T + b_ih
-    + b_hh (n, T, 4U), W_hh, the initial state and the optional per-step state mask;
-    outputs the hidden sequence (n, T, U) and the final cell state (n, U)."""
+class _LSTMSequences(torch.autograd.Function):
+    """k independent whole-sequence LSTM recurrences (same length T and unit count) in ONE
+    swarm_lstm_seq_forward_batch / _backward_batch launch each way (include/swarmtrain.h).
+    Arguments: k, then per problem the gate pre-activations xg = x W_ih^T + b_ih + b_hh
+    (n, T, 4U), W_hh, the initial state h0, c0 (n, U) and the optional per-step state mask
+    keep (n, T). Returns per problem the hidden sequence (n, T, U) and the final cell
+    state (n, U)."""
 
     @staticmethod
-    def forward(ctx, xg, w_hh, h0, c0, keep):
-        n, T, G = xg.shape
+    def forward(ctx, k, *args):
+        probs = [args[5 * i:5 * i + 5] for i in range(k)]
+        xg0 = probs[0][0]
+        T, G = xg0.shape[1], xg0.shape[2]
         U = G // 4
-        h_out = torch.empty(n, T, U, dtype=xg.dtype, device=xg.device)
-        c_out = torch.empty_like(h_out)
-        act = torch.empty_like(xg)
+        outs, descs, saved = [], [], []
+        for xg, w_hh, h0, c0, keep in probs:
+            n = xg.shape[0]
+            h_out = torch.empty(n, T, U, dtype=xg.dtype, device=xg.device)
+            c_out = torch.empty_like(h_out)
+            act = torch.empty_like(xg)
+            descs.append(_native.LstmSeqFwd(n, _addr(xg), _addr(w_hh), _addr(h0), _addr(c0), _addr(keep),
+                                            _addr(h_out), _addr(c_out), _addr(act)))
+            saved += [w_hh, h0, c0, keep, h_out, c_out, act]
+        arr = (_native.LstmSeqFwd * k)(*descs)
         lib = _native.load()
-        stream = C.c_void_p(torch.cuda.current_stream(xg.device).cuda_stream)
-        _native.check(lib.swarm_lstm_seq_forward(n, T, U, _ptr(xg), _ptr(w_hh), _ptr(h0), _ptr(c0), _ptr(keep),
-                                                 _ptr(h_out), _ptr(c_out), _ptr(act), stream),
-                      "swarm_lstm_seq_forward")
-        ctx.save_for_backward(w_hh, h0, c0, keep, h_out, c_out, act)
-        return h_out, c_out[:, -1].contiguous()
+        stream = C.c_void_p(torch.cuda.current_stream(xg0.device).cuda_stream)
+        _native.check(lib.swarm_lstm_seq_forward_batch(k, T, U, C.cast(arr, C.c_void_p), stream),
+                      "swarm_lstm_seq_forward_batch")
+        for i in range(k):
+            h_out, c_out = saved[7 * i + 4], saved[7 * i + 5]
+            outs += [h_out, c_out[:, -1].contiguous()]     # after the launch that writes c_out
+        ctx.k = k
+        ctx.save_for_backward(*saved)
+        return tuple(outs)
 
     @staticmethod
-    def backward(ctx, dh_out, dc_n):
-        w_hh, h0, c0, keep, h_out, c_out, act = ctx.saved_tensors
-        n, T, U = h_out.shape
-        dxg = torch.empty_like(act)
-        dh0 = torch.empty_like(h0)
-        dc0 = torch.empty_like(c0)
+    def backward(ctx, *grads):
+        k = ctx.k
+        saved = ctx.saved_tensors
+        descs, res, keepalive = [], [], []
+        for i in range(k):
+            w_hh, h0, c0, keep, h_out, c_out, act = saved[7 * i:7 * i + 7]
+            dh_out, dc_n = grads[2 * i].contiguous(), grads[2 * i + 1].contiguous()
+            dxg = torch.empty_like(act)
+            dh0, dc0 = torch.empty_like(h0), torch.empty_like(c0)
+            descs.append(_native.LstmSeqBwd(h_out.shape[0], _addr(w_hh), _addr(c0), _addr(keep), _addr(c_out),
+                                            _addr(act), _addr(dh_out), None, _addr(dc_n), _addr(dxg), _addr(dh0),
+                                            _addr(dc0)))
+            keepalive += [dh_out, dc_n]
+            res.append((dxg, dh0, dc0))
+        n0, T, U = saved[4].shape
+        arr = (_native.LstmSeqBwd * k)(*descs)
         lib = _native.load()
-        stream = C.c_void_p(torch.cuda.current_stream(act.device).cuda_stream)
-        _native.check(lib.swarm_lstm_seq_backward(n, T, U, _ptr(w_hh), _ptr(c0), _ptr(keep), _ptr(c_out), _ptr(act),
-                                                  _ptr(dh_out.contiguous()), None, _ptr(dc_n.contiguous()),
-                                                  _ptr(dxg), _ptr(dh0), _ptr(dc0), stream),
-                      "swarm_lstm_seq_backward")
-        dw = None
-        if ctx.needs_input_grad[1]:
-            # W_hh's gradient: dgates^T h_prev' over every (sequence, step) row, one GEMM
-            prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
-            h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
-            dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
-        return dxg, dw, dh0, dc0, None
+        stream = C.c_void_p(torch.cuda.current_stream(saved[4].device).cuda_stream)
+        _native.check(lib.swarm_lstm_seq_backward_batch(k, T, U, C.cast(arr, C.c_void_p), stream),
+                      "swarm_lstm_seq_backward_batch")
+        out = [None]
+        for i in range(k):
+            w_hh, h0, c0, keep, h_out, c_out, act = saved[7 * i:7 * i + 7]
+            dxg, dh0, dc0 = res[i]
+            dw = None
+            if ctx.needs_input_grad[1 + 5 * i + 1]:
+                # W_hh's gradient: dgates^T h_prev' over every (sequence, step) row, one GEMM
+                prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
+                h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
+                dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
+            out += [dxg, dw, dh0, dc0, None]
+        return tuple(out)
+
+
+def _addr(t):
+    return t.data_ptr() if t is not None else None
 
 
 class _AttnCore(torch.autograd.Function):
@@ -212,16 +243,46 @@ def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | 
     whose episode ended (poca_trainer.py:706-723, option_critic_trainer.py:496-506).
     On the GPU the recurrence is one swarm_lstm_seq_* launch each way (autograd
     supported); elsewhere the reference's loop of nn.LSTM calls."""
+    return lstm_sequences([(lstm, seq, state, keep)])[0]
+
+
+def _fused_seq_ok(lstm: nn.LSTM, seq: torch.Tensor) -> bool:
+    return (FUSED_LSTM and seq.is_cuda and _plain_lstm(lstm) and lstm.hidden_size <= _native.LSTM_SEQ_MAX_UNITS
+            and seq.dtype == torch.float32)
+
+
+def lstm_sequences(items):
+    """[lstm_sequence(lstm, seq, state, keep) for each item] with the GPU recurrences of items
+    that share a sequence length and unit count in ONE launch each way (_LSTMSequences): the
+    actor's and the critics' memories of a minibatch are independent, and one launch runs
+    their latency-bound chains side by side instead of back to back."""
+    out = [None] * len(items)
+    groups: dict = {}
+    for i, (lstm, seq, state, keep) in enumerate(items):
+        if _fused_seq_ok(lstm, seq):
+            groups.setdefault((seq.shape[1], lstm.hidden_size, seq.device), []).append(i)
+        else:
+            out[i] = _lstm_loop(lstm, seq, state, keep)
+    for idx in groups.values():
+        for chunk in (idx[j:j + _native.LSTM_MAX_BATCH] for j in range(0, len(idx), _native.LSTM_MAX_BATCH)):
+            args = []
+            for i in chunk:
+                lstm, seq, state, keep = items[i]
+                n, units = seq.shape[0], lstm.hidden_size
+                xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
+                args += [xg.contiguous(), lstm.weight_hh_l0.contiguous(), state[0].reshape(n, units).contiguous(),
+                         state[1].reshape(n, units).contiguous(),
+                         keep.to(torch.float32).contiguous() if keep is not None else None]
+            res = _LSTMSequences.apply(len(chunk), *args)
+            for j, i in enumerate(chunk):
+                h_seq, c_n = res[2 * j], res[2 * j + 1]
+                out[i] = (h_seq, (h_seq[:, -1].unsqueeze(0), c_n.unsqueeze(0)))
+    return out
+
+
+def _lstm_loop(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
+    """The reference's path: nn.LSTM over the sequence, or its per-step masked loop."""
     n, T, _ = seq.shape
-    units = lstm.hidden_size
-    if (FUSED_LSTM and seq.is_cuda and _plain_lstm(lstm) and units <= _native.LSTM_SEQ_MAX_UNITS
-            and seq.dtype == torch.float32):
-        xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
-        h0 = state[0].reshape(n, units).contiguous()
-        c0 = state[1].reshape(n, units).contiguous()
-        k = keep.to(torch.float32).contiguous() if keep is not None else None
-        out, c_n = _LSTMSequence.apply(xg.contiguous(), lstm.weight_hh_l0.contiguous(), h0, c0, k)
-        return out, (out[:, -1].unsqueeze(0), c_n.unsqueeze(0))
     if keep is None:
         return lstm(seq, state)
     outs = []
@@ -232,6 +293,24 @@ def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | 
             k = keep[:, t].reshape(1, n, 1).to(o.dtype)
             state = (state[0] * k, state[1] * k)
     return torch.cat(outs, dim=1), state
+
+
+def batched_sequence_passes(requests, extra_items=()):
+    """POCACritic.sequence_passes of several critics (requests: (critic, all_states,
+    all_actions, focal_agent_ids, memories, sequence_length, passes) each) with all their
+    memories, and any `extra_items` (other independent LSTM items), in ONE LSTM launch each
+    way. Returns (the values of each request, the outputs of the extra items)."""
+    begun = [req[0].sequence_passes_begin(*req[1:]) for req in requests]
+    items = [it for it, _ in begun if it is not None] + list(extra_items)
+    outs = lstm_sequences(items) if items else []
+    values, j = [], 0
+    for (critic, *_), (it, ctx) in zip(requests, begun):
+        lstm_out = None
+        if it is not None:
+            lstm_out = outs[j][0]
+            j += 1
+        values.append(critic.sequence_passes_end(lstm_out, ctx))
+    return values, outs[j:]
 
 
 def _lstm(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
@@ -361,11 +440,16 @@ class RecurrentDiscreteActor(nn.Module):
     def forward_sequence(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
         """(B, T, obs) -> logits (B, T, A), memory. keep (B, T): the memory is multiplied by
         keep[:, t] after step t (the trainer's per-step episode-end resets)."""
+        out, nxt = _lstm(*self.sequence_lstm_item(obs_seq, state, keep))
+        return self.logits_head(out), nxt
+
+    def sequence_lstm_item(self, obs_seq: torch.Tensor, state=None, keep: torch.Tensor | None = None):
+        """forward_sequence up to its LSTM: (lstm, encoded sequence, state, keep), for
+        lstm_sequences to run together with other independent memories; the logits are
+        logits_head(the LSTM output)."""
         B, T = obs_seq.shape[:2]
         enc = self.net(obs_seq.reshape(B * T, self.obs_dim)).view(B, T, -1)
-        out, nxt = _lstm(self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device),
-                         keep)
-        return self.logits_head(out), nxt
+        return self.lstm, enc, state if state is not None else self.initial_state(B, obs_seq.device), keep
 
     def step(self, obs: torch.Tensor, state=None):
         logits, nxt = self.forward_sequence(obs.unsqueeze(1), state)
@@ -529,19 +613,32 @@ class POCACritic(nn.Module):
     def _value_tail(self, pooled, n_agents, memory=None, sequence_length=1, return_memory=False):
         """linear encoder -> [LSTM] -> agent count -> value head (poca_networks.py:608-625)."""
         B = pooled.shape[0]
-        encoding = self.linear_encoder(pooled)
+        encoding, item = self._tail_begin(pooled, memory, sequence_length)
         next_memory = memory
-        if self.lstm is not None:
-            sequence_length = int(sequence_length)
-            if sequence_length <= 0 or B % sequence_length:
-                raise ValueError("Critic batch must be divisible by sequence_length")
-            n_seq = B // sequence_length
-            seq, next_memory = _lstm(self.lstm, encoding.view(n_seq, sequence_length, self.h_size),
-                                         memory if memory is not None else self.initial_state(n_seq, encoding.device))
+        if item is not None:
+            seq, next_memory = _lstm(*item)
             encoding = seq.reshape(B, self.hidden_size)
-        encoding = torch.cat([encoding, self._norm_agent_count(n_agents, B, encoding.device)], dim=-1)
-        value = self.value_head(encoding)
+        value = self._tail_end(encoding, n_agents)
         return (value, next_memory) if return_memory else value
+
+    def _tail_begin(self, pooled, memory=None, sequence_length=1):
+        """The value tail up to its LSTM: (encoding, LSTM item (lstm, sequences, state, None)
+        or None without a memory)."""
+        B = pooled.shape[0]
+        encoding = self.linear_encoder(pooled)
+        if self.lstm is None:
+            return encoding, None
+        sequence_length = int(sequence_length)
+        if sequence_length <= 0 or B % sequence_length:
+            raise ValueError("Critic batch must be divisible by sequence_length")
+        n_seq = B // sequence_length
+        return encoding, (self.lstm, encoding.view(n_seq, sequence_length, self.h_size),
+                          memory if memory is not None else self.initial_state(n_seq, encoding.device), None)
+
+    def _tail_end(self, encoding, n_agents):
+        B = encoding.shape[0]
+        encoding = torch.cat([encoding, self._norm_agent_count(n_agents, B, encoding.device)], dim=-1)
+        return self.value_head(encoding)
 
     def _encode_and_value(self, entities, n_agents, memory=None, sequence_length=1, return_memory=False):
         """RSA -> tail on explicit entity sets (B, n, h) (poca_networks.py:597-625)."""
@@ -647,6 +744,15 @@ class POCACritic(nn.Module):
         unchanged (up to GEMM summation order): one attention, one encoder, ONE LSTM launch over
         all passes' sequences and one head instead of one of each per pass. Returns the (B,)
         values of each pass in `passes` order."""
+        item, ctx = self.sequence_passes_begin(all_states, all_actions, focal_agent_ids, memories, sequence_length,
+                                               passes)
+        return self.sequence_passes_end(_lstm(*item)[0] if item is not None else None, ctx)
+
+    def sequence_passes_begin(self, all_states, all_actions, focal_agent_ids, memories: dict, sequence_length: int,
+                              passes=("value", "baseline")):
+        """sequence_passes up to its LSTM: (LSTM item (lstm, sequences, state, None) or None,
+        context for sequence_passes_end). With lstm_sequences the item runs in the same launch
+        as other independent memories (the actor's)."""
         B, N, _ = all_states.shape
         sets = []
         for name in passes:
@@ -663,8 +769,15 @@ class POCACritic(nn.Module):
         if self.lstm is not None:
             memory = tuple(torch.cat([memories[name][i] for name in passes], dim=1) for i in (0, 1))
         pooled = self.self_attn(ents)
-        values = self._value_tail(pooled, N, memory, sequence_length).squeeze(-1)
-        return list(values.split(B))
+        encoding, item = self._tail_begin(pooled, memory, sequence_length)
+        return item, (encoding, N, B)
+
+    def sequence_passes_end(self, lstm_out, ctx):
+        """The values of sequence_passes from the LSTM output of its item (None without memory)."""
+        encoding, N, B = ctx
+        if lstm_out is not None:
+            encoding = lstm_out.reshape(encoding.shape[0], self.hidden_size)
+        return list(self._tail_end(encoding, N).squeeze(-1).split(B))
 
     def decision_passes(self, all_states, all_actions, *, value: bool = True, joint: bool = False,
                         baselines: bool = True, value_memory=None, joint_memory=None, baseline_memory=None):

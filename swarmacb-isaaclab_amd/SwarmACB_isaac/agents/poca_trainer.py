@@ -35,7 +35,7 @@ from .checkpoint import load_poca_checkpoint, poca_checkpoint
 from .collector import POCARolloutCollector
 from .config import POCAConfig
 from .poca_buffer import POCARolloutBuffer
-from .poca_networks import Actor, DiscreteActor, POCACritic, RecurrentDiscreteActor
+from .poca_networks import Actor, DiscreteActor, POCACritic, RecurrentDiscreteActor, lstm_sequences
 
 __all__ = ["POCAConfig", "POCATrainer", "PolynomialDecay", "masked_mean", "trust_region_policy_loss",
            "trust_region_value_loss"]
@@ -141,17 +141,22 @@ class POCATrainer(TrainerBase):
                                                 denom=d_row)
         return policy_loss, value_loss, baseline_loss, mean_entropy
 
-    def _actor_sequence(self, batch: dict):
+    def _actor_sequence(self, batch: dict, other_item=None):
         """The recurrent actor over the minibatch sequences with the memory of rows whose
         episode ended at t zeroed before step t+1 (the per-step loop of PT:706-723, as one
-        masked sequence: one swarm_lstm_seq launch each way on the GPU)."""
+        masked sequence: one swarm_lstm_seq launch each way on the GPU). `other_item`: an
+        independent LSTM item (the critic's) run in the same launch; its output is returned."""
         obs, actions = batch["obs"], batch["actions"]
         B, L = obs.shape[:2]
         state = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
-        logits, _ = self.actor.forward_sequence(obs, state, keep=1.0 - batch["dones"])
+        items = [self.actor.sequence_lstm_item(obs, state, keep=1.0 - batch["dones"])]
+        if other_item is not None:
+            items.append(other_item)
+        outs = lstm_sequences(items)
+        logits = self.actor.logits_head(outs[0][0])
         dist = torch.distributions.Categorical(validate_args=False, logits=logits.reshape(B * L, -1))
         logp = dist.log_prob(actions.reshape(B * L).long()).view(B, L, 1)
-        return logp, dist.entropy().view(B, L)
+        return logp, dist.entropy().view(B, L), (outs[1][0] if other_item is not None else None)
 
     def _compute_recurrent_losses(self, batch: dict, current_eps: float):
         """poca_trainer.py:690-775."""
@@ -159,24 +164,26 @@ class POCATrainer(TrainerBase):
         loss_mask = batch["loss_mask"].bool()
         B, L = batch["obs"].shape[:2]
         N = critic_states.shape[2]
-        logp_seq, ent_seq = self._actor_sequence(batch)
+        flat_states = critic_states.reshape(B * L, N, critic_states.shape[-1])
+        flat_actions = batch["critic_actions"].reshape(B * L, N, batch["critic_actions"].shape[-1])
+        critic_act = self._encode_actions_for_critic(flat_actions)
+        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
+        # critic_pass and focal_baselines (PT:748-770) as one batched pass (POCACritic.sequence_passes),
+        # whose memory runs in the same LSTM launch as the actor's (lstm_sequences)
+        c_item, c_ctx = self.critic.sequence_passes_begin(
+            flat_states, critic_act, focal_ids,
+            {"value": (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
+             "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
+                          batch["baseline_memory_c"].unsqueeze(0).detach())},
+            sequence_length=L, passes=("value", "baseline"))
+        logp_seq, ent_seq, c_out = self._actor_sequence(batch, c_item)
+        new_tv, new_bl = self.critic.sequence_passes_end(c_out, c_ctx)
         (d_mask,) = self._denominators([loss_mask.sum()])
         policy_loss = trust_region_policy_loss(batch["advantages"].unsqueeze(-1).reshape(-1, 1),
                                                logp_seq.reshape(-1, logp_seq.shape[-1]),
                                                batch["old_log_probs"].reshape(-1, batch["old_log_probs"].shape[-1]),
                                                current_eps, loss_mask.reshape(-1), denom=d_mask)
         mean_entropy = (ent_seq * loss_mask).sum() / (d_mask if d_mask is not None else loss_mask.sum().clamp_min(1))
-        flat_states = critic_states.reshape(B * L, N, critic_states.shape[-1])
-        flat_actions = batch["critic_actions"].reshape(B * L, N, batch["critic_actions"].shape[-1])
-        critic_act = self._encode_actions_for_critic(flat_actions)
-        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        # critic_pass and focal_baselines (PT:748-770) as one batched pass (POCACritic.sequence_passes)
-        new_tv, new_bl = self.critic.sequence_passes(
-            flat_states, critic_act, focal_ids,
-            {"value": (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
-             "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
-                          batch["baseline_memory_c"].unsqueeze(0).detach())},
-            sequence_length=L, passes=("value", "baseline"))
         flat_mask = loss_mask.reshape(B * L)
         value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
                                              batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)

@@ -36,6 +36,36 @@ __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(
 constexpr int PF = 8;
 constexpr int PB = 4;
 
+// Several independent recurrences in ONE launch (swarm_lstm_seq_*_batch): workgroup
+// blockIdx.x belongs to the problem whose range [first[k], first[k + 1]) holds it. A
+// problem without a keep mask reads the constant 1 (keep stride 0), so the mask costs no
+// branch around a load.
+constexpr int MAXB = SWARM_LSTM_MAX_BATCH;
+struct FwdSeq {
+    const float *xg, *w_hh, *h0, *c0, *keep;
+    float *h_out, *c_out, *act;
+    int32_t ks;   // keep stride: 1, or 0 with keep -> the constant 1
+};
+struct BwdSeq {
+    const float *w_hh, *c0, *keep, *c_out, *act, *dh_out, *dh_n, *dc_n;
+    float *dxg, *dh0, *dc0;
+    int32_t ks;
+};
+template <class S>
+struct Batch {
+    int32_t count;
+    int32_t first[MAXB + 1];
+    S s[MAXB];
+};
+template <class S>
+__device__ __forceinline__ int batch_item(const Batch<S>& bt, int blk) {
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < MAXB; ++i) k += (i < bt.count && blk >= bt.first[i]) ? 1 : 0;
+    return k;
+}
+__device__ float g_keep_one[1] = {1.0f};
+
 // Activations from the hardware exponential and reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp
 // each) instead of the library's expf / tanhf / IEEE division, which dominated the
 // per-step chain; tanh(x) = 2 sigmoid(2x) - 1 (absolute error ~1e-7 near 0).
@@ -56,16 +86,22 @@ __device__ __forceinline__ float lane_bcast(float v, int k) {
 // by step parity) and ONE barrier. Per step: U readlanes + U FMAs (4 chains) per lane,
 // one activation, one LDS write / barrier / read, one cell update.
 template <int UC, bool KEEP>
-__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const float* __restrict__ xg,
-                                                          const float* __restrict__ w_hh,
-                                                          const float* __restrict__ h0,
-                                                          const float* __restrict__ c0,
-                                                          const float* __restrict__ keep, float* __restrict__ h_out,
-                                                          float* __restrict__ c_out, float* __restrict__ act) {
+__global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const Batch<FwdSeq> bt) {
     constexpr int KU = UC > 0 ? UC : MAXU;              // register extent of a gate row
     const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float gs[2][4 * MAXU];
-    const int64_t b = blockIdx.x;
+    const int item = batch_item(bt, blockIdx.x);
+    const FwdSeq& sq = bt.s[item];
+    const float* __restrict__ xg = sq.xg;
+    const float* __restrict__ w_hh = sq.w_hh;
+    const float* __restrict__ h0 = sq.h0;
+    const float* __restrict__ c0 = sq.c0;
+    const float* __restrict__ keep = sq.keep;
+    float* __restrict__ h_out = sq.h_out;
+    float* __restrict__ c_out = sq.c_out;
+    float* __restrict__ act = sq.act;
+    const int64_t ks = sq.ks;
+    const int64_t b = (int64_t)blockIdx.x - bt.first[item];
     const int j = threadIdx.x;
     const int wave = j >> 6, lane = j & 63;
     const int G = 4 * U;
@@ -84,7 +120,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
         for (int p = 0; p < PF; ++p) {
             const int t = min(t0 + p, T - 1);
             xr[p] = xb[(int64_t)t * G];
-            if constexpr (KEEP) kr[p] = keep[b * T + t];
+            if constexpr (KEEP) kr[p] = keep[(b * T + t) * ks];
         }
     };
     float xr[PF], kr[PF] = {};
@@ -141,20 +177,26 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
 }
 
 template <int UC, bool KEEP>
-__global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const float* __restrict__ w_hh,
-                                                          const float* __restrict__ c0,
-                                                          const float* __restrict__ keep,
-                                                          const float* __restrict__ c_out,
-                                                          const float* __restrict__ act,
-                                                          const float* __restrict__ dh_out,
-                                                          const float* __restrict__ dh_n,
-                                                          const float* __restrict__ dc_n, float* __restrict__ dxg,
-                                                          float* __restrict__ dh0, float* __restrict__ dc0) {
+__global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const Batch<BwdSeq> bt) {
     constexpr int KU = UC > 0 ? UC : MAXU;
     const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float dgs[4 * MAXU];
     __shared__ __attribute__((aligned(16))) float part[4 * MAXU];
-    const int64_t b = blockIdx.x;
+    const int item = batch_item(bt, blockIdx.x);
+    const BwdSeq& sq = bt.s[item];
+    const float* __restrict__ w_hh = sq.w_hh;
+    const float* __restrict__ c0 = sq.c0;
+    const float* __restrict__ keep = sq.keep;
+    const float* __restrict__ c_out = sq.c_out;
+    const float* __restrict__ act = sq.act;
+    const float* __restrict__ dh_out = sq.dh_out;
+    const float* __restrict__ dh_n = sq.dh_n;
+    const float* __restrict__ dc_n = sq.dc_n;
+    float* __restrict__ dxg = sq.dxg;
+    float* __restrict__ dh0 = sq.dh0;
+    float* __restrict__ dc0 = sq.dc0;
+    const int64_t ks = sq.ks;
+    const int64_t b = (int64_t)blockIdx.x - bt.first[item];
     const int j = threadIdx.x;
     const int G = 4 * U;
     // thread j < G is gate row j = q U + u in phase 1 (its gate's gradient) and, in phase 2,
@@ -185,7 +227,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
         v.gg = a[2 * U + u];
         v.og = a[3 * U + u];
         v.ct = c_out[row * U + u];
-        const float kp = KEEP ? keep[rp] : 1.0f;
+        const float kp = KEEP ? keep[rp * ks] : 1.0f;
         v.kprev = t > 0 ? kp : 1.0f;
         const float cpv = c_out[rp * U + u];
         v.cp = t > 0 ? cpv : c0u;
@@ -259,17 +301,13 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
 }
 
 template <int UC, bool KEEP>
-void launch_fwd(int64_t n, int T, int U, const float* xg, const float* w_hh, const float* h0, const float* c0,
-                const float* keep, float* h_out, float* c_out, float* act, hipStream_t st) {
-    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, xg, w_hh, h0, c0, keep, h_out, c_out, act);
+void launch_fwd(int64_t n, int T, int U, const Batch<FwdSeq>& bt, hipStream_t st) {
+    lstm_seq_fwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, bt);
 }
 
 template <int UC, bool KEEP>
-void launch_bwd(int64_t n, int T, int U, const float* w_hh, const float* c0, const float* keep, const float* c_out,
-                const float* act, const float* dh_out, const float* dh_n, const float* dc_n, float* dxg, float* dh0,
-                float* dc0, hipStream_t st) {
-    lstm_seq_bwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n,
-                                                              dxg, dh0, dc0);
+void launch_bwd(int64_t n, int T, int U, const Batch<BwdSeq>& bt, hipStream_t st) {
+    lstm_seq_bwd_kernel<UC, KEEP><<<(unsigned)n, NT, 0, st>>>(T, U, bt);
 }
 
 // the unit counts of the reference's configs (memory 128 -> 64, 64 -> 32, ...) compile
@@ -288,41 +326,102 @@ bool args_ok(int64_t n, int32_t T, int32_t units) {
     return n >= 0 && n <= 0x7fffffff && T >= 1 && units >= 1 && units <= MAXU;
 }
 
+const float* keep_one() {
+    static const float* p = [] {
+        void* q = nullptr;
+        return hipGetSymbolAddress(&q, HIP_SYMBOL(g_keep_one)) == hipSuccess ? static_cast<const float*>(q) : nullptr;
+    }();
+    return p;
+}
+
+// shared checks of the batch entry points: per-problem sizes and pointers, prefix ranges
+template <class In, class Ok>
+int32_t build_batch(int32_t count, int32_t T, int32_t units, const In* seqs, Ok ok, int64_t& total, bool& any_keep,
+                    int32_t* first) {
+    if (count < 1 || count > MAXB || !seqs || T < 1 || units < 1 || units > MAXU) return SWARM_ERR_ARG;
+    total = 0;
+    any_keep = false;
+    for (int k = 0; k < count; ++k) {
+        if (!args_ok(seqs[k].n, T, units) || (seqs[k].n > 0 && !ok(seqs[k]))) return SWARM_ERR_ARG;
+        first[k] = (int32_t)total;
+        total += seqs[k].n;
+        any_keep |= seqs[k].keep != nullptr;
+    }
+    if (total > 0x7fffffff) return SWARM_ERR_ARG;
+    first[count] = (int32_t)total;
+    return SWARM_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
+int32_t swarm_lstm_seq_forward_batch(int32_t count, int32_t T, int32_t units, const swarm_lstm_seq_fwd_t* seqs,
+                                     void* stream) {
+    Batch<FwdSeq> bt{};
+    int64_t total;
+    bool any_keep;
+    const int32_t rc = build_batch(count, T, units, seqs, [](const swarm_lstm_seq_fwd_t& q) {
+        return q.xg && q.w_hh && q.h0 && q.c0 && q.h_out && q.c_out && q.act;
+    }, total, any_keep, bt.first);
+    if (rc != SWARM_OK) return rc;
+    if (total == 0) return SWARM_OK;
+    const float* one = keep_one();
+    if (any_keep && !one) return swarm::record_hip_status();
+    bt.count = count;
+    for (int k = 0; k < count; ++k) {
+        const swarm_lstm_seq_fwd_t& q = seqs[k];
+        bt.s[k] = FwdSeq{q.xg, q.w_hh, q.h0, q.c0, q.keep ? q.keep : one, q.h_out, q.c_out, q.act, q.keep ? 1 : 0};
+    }
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (any_keep) {
+        SWARM_LSTM_DISPATCH(launch_fwd, true, total, T, units, bt, st)
+    } else {
+        SWARM_LSTM_DISPATCH(launch_fwd, false, total, T, units, bt, st)
+    }
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_lstm_seq_backward_batch(int32_t count, int32_t T, int32_t units, const swarm_lstm_seq_bwd_t* seqs,
+                                      void* stream) {
+    Batch<BwdSeq> bt{};
+    int64_t total;
+    bool any_keep;
+    const int32_t rc = build_batch(count, T, units, seqs, [](const swarm_lstm_seq_bwd_t& q) {
+        return q.w_hh && q.c0 && q.c_out && q.act && q.dh_out && q.dxg;
+    }, total, any_keep, bt.first);
+    if (rc != SWARM_OK) return rc;
+    if (total == 0) return SWARM_OK;
+    const float* one = keep_one();
+    if (any_keep && !one) return swarm::record_hip_status();
+    bt.count = count;
+    for (int k = 0; k < count; ++k) {
+        const swarm_lstm_seq_bwd_t& q = seqs[k];
+        bt.s[k] = BwdSeq{q.w_hh, q.c0, q.keep ? q.keep : one, q.c_out, q.act, q.dh_out, q.dh_n, q.dc_n,
+                         q.dxg, q.dh0, q.dc0, q.keep ? 1 : 0};
+    }
+    const hipStream_t st = static_cast<hipStream_t>(stream);
+    if (any_keep) {
+        SWARM_LSTM_DISPATCH(launch_bwd, true, total, T, units, bt, st)
+    } else {
+        SWARM_LSTM_DISPATCH(launch_bwd, false, total, T, units, bt, st)
+    }
+    return swarm::record_hip_status();
+}
+
 int32_t swarm_lstm_seq_forward(int64_t n, int32_t T, int32_t units, const float* xg, const float* w_hh,
                                const float* h0, const float* c0, const float* keep, float* h_out, float* c_out,
                                float* act, void* stream) {
-    if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
-    if (n == 0) return SWARM_OK;
-    if (!xg || !w_hh || !h0 || !c0 || !h_out || !c_out || !act) return SWARM_ERR_ARG;
-    const hipStream_t st = static_cast<hipStream_t>(stream);
-    if (keep) {
-        SWARM_LSTM_DISPATCH(launch_fwd, true, n, T, units, xg, w_hh, h0, c0, keep, h_out, c_out, act, st)
-    } else {
-        SWARM_LSTM_DISPATCH(launch_fwd, false, n, T, units, xg, w_hh, h0, c0, keep, h_out, c_out, act, st)
-    }
-    return swarm::record_hip_status();
+    const swarm_lstm_seq_fwd_t q{n, xg, w_hh, h0, c0, keep, h_out, c_out, act};
+    return swarm_lstm_seq_forward_batch(1, T, units, &q, stream);
 }
 
 int32_t swarm_lstm_seq_backward(int64_t n, int32_t T, int32_t units, const float* w_hh, const float* c0,
                                 const float* keep, const float* c_out, const float* act, const float* dh_out,
                                 const float* dh_n, const float* dc_n, float* dxg, float* dh0, float* dc0,
                                 void* stream) {
-    if (!args_ok(n, T, units)) return SWARM_ERR_ARG;
-    if (n == 0) return SWARM_OK;
-    if (!w_hh || !c0 || !c_out || !act || !dh_out || !dxg) return SWARM_ERR_ARG;
-    const hipStream_t st = static_cast<hipStream_t>(stream);
-    if (keep) {
-        SWARM_LSTM_DISPATCH(launch_bwd, true, n, T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0,
-                            dc0, st)
-    } else {
-        SWARM_LSTM_DISPATCH(launch_bwd, false, n, T, units, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0,
-                            dc0, st)
-    }
-    return swarm::record_hip_status();
+    const swarm_lstm_seq_bwd_t q{n, w_hh, c0, keep, c_out, act, dh_out, dh_n, dc_n, dxg, dh0, dc0};
+    return swarm_lstm_seq_backward_batch(1, T, units, &q, stream);
 }
 
 }  // extern "C"

@@ -68,3 +68,37 @@ def test_lstm_sequence_rejects_wide_units(gpu_device):
     outs_k, _ = _run(True, *case)
     outs_t, _ = _run(False, *case)
     torch.testing.assert_close(outs_k[0], outs_t[0])
+
+
+def test_lstm_sequences_batch_equals_single_launches(gpu_device):
+    """lstm_sequences: three independent recurrences (different sequence counts, with and
+    without the keep mask) in one swarm_lstm_seq_*_batch launch each way give bit for bit
+    the outputs and gradients of one launch per recurrence."""
+    cases = [_case(16, 128, 128, 64, True, gpu_device, seed=1), _case(40, 128, 128, 64, False, gpu_device, seed=2),
+             _case(7, 128, 64, 64, True, gpu_device, seed=3)]
+
+    def run(batched):
+        for lstm, *_ in cases:
+            lstm.zero_grad()
+        ins = [[t.clone().requires_grad_(True) for t in (x, h0, c0)] for _, x, h0, c0, _, _ in cases]
+        items = [(c[0], i[0], (i[1], i[2]), c[4]) for c, i in zip(cases, ins)]
+        res = PN.lstm_sequences(items) if batched else [PN.lstm_sequence(*it) for it in items]
+        loss = sum((out * c[5]).sum() + (hn ** 2).sum() + (cn * 0.3).sum() for (out, (hn, cn)), c in zip(res, cases))
+        loss.backward()
+        outs = [t.detach() for out, (hn, cn) in res for t in (out, hn, cn)]
+        grads = [t.grad for i in ins for t in i] + [p.grad.clone() for c in cases for p in c[0].parameters()]
+        return outs, grads
+
+    outs_b, grads_b = run(True)
+    outs_s, grads_s = run(False)
+    for a, b in zip(outs_b + grads_b, outs_s + grads_s):
+        assert torch.equal(a, b)
+
+
+def test_lstm_batch_rejects_bad_counts(gpu_device):
+    from SwarmACB_isaac import _native
+
+    lib = _native.load()
+    assert lib.swarm_lstm_seq_forward_batch(0, 8, 64, None, None) == -1
+    assert lib.swarm_lstm_seq_forward_batch(_native.LSTM_MAX_BATCH + 1, 8, 64, None, None) == -1
+    assert lib.swarm_lstm_seq_backward_batch(1, 8, 65, None, None) == -1
