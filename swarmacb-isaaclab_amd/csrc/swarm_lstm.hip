@@ -182,6 +182,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
     const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float dgs[4 * MAXU];
     __shared__ __attribute__((aligned(16))) float part[4 * MAXU];
+    __shared__ __attribute__((aligned(16))) float partb[2][4 * MAXU];   // UC == MAXU path
     const int item = batch_item(bt, blockIdx.x);
     const BwdSeq& sq = bt.s[item];
     const float* __restrict__ w_hh = sq.w_hh;
@@ -249,6 +250,44 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
             if (t < 0) break;
             const int64_t row = b * T + t;
             const StepIn in = cur[p];
+            if constexpr (UC == MAXU) {
+                // 64 units: wave q = gate quarter q, lane m = unit m, so the phase-2 inputs of
+                // thread (q, u) -- the gate gradients of rows q U + m -- are lane m's phase-1
+                // result in the SAME wave: broadcast by v_readlane, no LDS round trip and no
+                // barrier between the phases; the 4 quarter partials of a unit meet in LDS
+                // (double-buffered by step parity) behind ONE barrier per step.
+                const float* pin = partb[(t + 1) & 1];
+                if (t < T - 1)
+                    dh_rec = ((pin[u] + pin[U + u]) + (pin[2 * U + u] + pin[3 * U + u])) * k_after;
+                const float cp = t > 0 ? in.cp * in.kprev : in.cp;
+                const float dh = in.dh + dh_rec;
+                const float tc = tanhf(in.ct);
+                const float dc = dc_rec + dh * in.og * (1.0f - tc * tc);
+                float gq;
+                if (q == 0) gq = dc * in.gg * in.ig * (1.0f - in.ig);
+                else if (q == 1) gq = dc * cp * in.fg * (1.0f - in.fg);
+                else if (q == 2) gq = dc * in.ig * (1.0f - in.gg * in.gg);
+                else gq = dh * tc * in.og * (1.0f - in.og);
+                dxg[row * G + j] = gq;
+                dc_prev = dc * in.fg;
+                dc_rec = dc_prev * in.kprev;
+                k_after = in.kprev;
+                float gk[KU];
+#pragma unroll
+                for (int m = 0; m < KU; ++m) gk[m] = lane_bcast(gq, m);
+                __builtin_amdgcn_sched_barrier(0);
+                float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+                for (int m = 0; m < KU; m += 4) {
+                    s0 = fmaf(wt[m], gk[m], s0);
+                    s1 = fmaf(wt[m + 1], gk[m + 1], s1);
+                    s2 = fmaf(wt[m + 2], gk[m + 2], s2);
+                    s3 = fmaf(wt[m + 3], gk[m + 3], s3);
+                }
+                partb[t & 1][j] = (s0 + s1) + (s2 + s3);
+                __syncthreads();
+                continue;
+            }
             if (act_j) {
                 if (t < T - 1)   // dh_prev' of step t + 1, masked by the keep between t and t + 1
                     dh_rec = ((part[u] + part[U + u]) + (part[2 * U + u] + part[3 * U + u])) * k_after;
@@ -295,7 +334,8 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
         for (int p = 0; p < PB; ++p) cur[p] = nx[p];
     }
     if (j < U) {
-        if (dh0) dh0[b * U + j] = (part[j] + part[U + j]) + (part[2 * U + j] + part[3 * U + j]);
+        const float* pl = UC == MAXU ? partb[0] : part;   // the step-0 partials
+        if (dh0) dh0[b * U + j] = (pl[j] + pl[U + j]) + (pl[2 * U + j] + pl[3 * U + j]);
         if (dc0) dc0[b * U + j] = dc_prev;
     }
 }
