@@ -105,6 +105,26 @@ int32_t swarm_rsa_attn_forward(int64_t S, int32_t N, int32_t H, int32_t D, const
 int32_t swarm_rsa_attn_backward(int64_t S, int32_t N, int32_t H, int32_t D, const float* qkv, const float* key_mask,
                                 const float* d_att, float* d_qkv, void* stream);
 
+/* The two LayerNorms (no affine, eps 1e-5) of ResidualSelfAttention under autograd (reference
+ * agents/poca_networks.py:417-491: x = embedding_norm(inp); out = residual_norm(fc_out(att) + x);
+ * pooled = out.mean(dim=1)), replacing torch's layer_norm / add / mean and their backwards in every
+ * PPO optimizer step. Rows are `width` (128 or 256) floats, 16-byte aligned, row-major.
+ *
+ * swarm_row_norm_forward: xhat[r] = (in[r] - mean) / sqrt(var + eps) (the normalised output) and
+ *   rstd[r] = 1 / sqrt(var + eps), for rows r < rows.
+ * swarm_row_norm_backward: dx = rstd * (dy - mean(dy) - xhat * mean(dy * xhat)) per row.
+ * swarm_set_pool_forward: per set s of n rows (row s*n + j): z = a + x, xhat = LayerNorm(z), rstd as
+ *   above, pooled[s] = mean_j xhat[s*n + j] — the residual add, the second LayerNorm and the mean in one pass.
+ * swarm_set_pool_backward: dz[s*n + j] = the LayerNorm backward of dpooled[s] / n (the mean's gradient),
+ *   i.e. the gradient of both a and x. */
+int32_t swarm_row_norm_forward(int64_t rows, int32_t width, const float* in, float* xhat, float* rstd, void* stream);
+int32_t swarm_row_norm_backward(int64_t rows, int32_t width, const float* dy, const float* xhat, const float* rstd,
+                                float* dx, void* stream);
+int32_t swarm_set_pool_forward(int64_t sets, int32_t n, int32_t width, const float* a, const float* x, float* xhat,
+                               float* rstd, float* pooled, void* stream);
+int32_t swarm_set_pool_backward(int64_t sets, int32_t n, int32_t width, const float* dpooled, const float* xhat,
+                                const float* rstd, float* dz, void* stream);
+
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
  * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.

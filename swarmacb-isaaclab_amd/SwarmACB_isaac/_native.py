@@ -71,7 +71,9 @@ class GatherField(C.Structure):
 CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
                  "swarm_rsa_attn_backward", "swarm_tensor_list_copy", "swarm_lstm_seq_forward_batch",
-                 "swarm_lstm_seq_backward_batch"]
+                 "swarm_lstm_seq_backward_batch", "swarm_row_norm_forward", "swarm_row_norm_backward",
+                 "swarm_set_pool_forward", "swarm_set_pool_backward"]
+NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 
 
@@ -174,6 +176,14 @@ def load() -> C.CDLL:
     lib.swarm_rsa_attn_backward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp, vp]
     lib.swarm_tensor_list_copy.restype = i32
     lib.swarm_tensor_list_copy.argtypes = [i32, vp, vp, vp, C.c_int64, vp, vp]
+    lib.swarm_row_norm_forward.restype = i32
+    lib.swarm_row_norm_forward.argtypes = [i64, i32, vp, vp, vp, vp]
+    lib.swarm_row_norm_backward.restype = i32
+    lib.swarm_row_norm_backward.argtypes = [i64, i32, vp, vp, vp, vp, vp]
+    lib.swarm_set_pool_forward.restype = i32
+    lib.swarm_set_pool_forward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp]
+    lib.swarm_set_pool_backward.restype = i32
+    lib.swarm_set_pool_backward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

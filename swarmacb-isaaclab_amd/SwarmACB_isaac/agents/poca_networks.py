@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -120,6 +121,8 @@ def _mlagents_lstm(input_size: int, memory_size: int, forget_bias: float = 1.0) 
 
 FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of the reference path)
 FUSED_ATTENTION = True   # False: ResidualSelfAttention's core runs torch's bmm / softmax path
+# False (or SWARM_FUSED_NORMS=0): its LayerNorms, residual add and set mean run torch's ops
+FUSED_NORMS = os.environ.get("SWARM_FUSED_NORMS", "1") != "0"
 
 
 def _plain_lstm(lstm: nn.LSTM) -> bool:
@@ -234,6 +237,64 @@ class _AttnCore(torch.autograd.Function):
                                                   _ptr(d_qkv), stream),
                       "swarm_rsa_attn_backward")
         return d_qkv, None, None, None, None
+
+
+class _RowNorm(torch.autograd.Function):
+    """LayerNorm without affine (eps 1e-5) of (rows, D) on swarm_row_norm_forward / _backward
+    (include/swarmtrain.h): the saved x_hat is the output itself, plus 1/std per row."""
+
+    @staticmethod
+    def forward(ctx, x):
+        rows, D = x.shape
+        xhat = torch.empty_like(x)
+        rstd = torch.empty(rows, dtype=x.dtype, device=x.device)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _native.check(lib.swarm_row_norm_forward(rows, D, _ptr(x), _ptr(xhat), _ptr(rstd), stream),
+                      "swarm_row_norm_forward")
+        ctx.save_for_backward(xhat, rstd)
+        return xhat
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, rstd = ctx.saved_tensors
+        dx = torch.empty_like(xhat)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(xhat.device).cuda_stream)
+        _native.check(lib.swarm_row_norm_backward(xhat.shape[0], xhat.shape[1], _ptr(dy.contiguous()), _ptr(xhat),
+                                                  _ptr(rstd), _ptr(dx), stream), "swarm_row_norm_backward")
+        return dx
+
+
+class _SetPool(torch.autograd.Function):
+    """LayerNorm(a + x).mean over each set of n rows (the residual tail of
+    ResidualSelfAttention, poca_networks.py:486-491) in one pass each way on
+    swarm_set_pool_forward / _backward: a, x (S*n, D) -> pooled (S, D)."""
+
+    @staticmethod
+    def forward(ctx, a, x, S: int, n: int):
+        D = a.shape[1]
+        xhat = torch.empty_like(a)
+        rstd = torch.empty(a.shape[0], dtype=a.dtype, device=a.device)
+        pooled = torch.empty(S, D, dtype=a.dtype, device=a.device)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(a.device).cuda_stream)
+        _native.check(lib.swarm_set_pool_forward(S, n, D, _ptr(a), _ptr(x), _ptr(xhat), _ptr(rstd), _ptr(pooled),
+                                                 stream), "swarm_set_pool_forward")
+        ctx.save_for_backward(xhat, rstd)
+        ctx.dims = (S, n)
+        return pooled
+
+    @staticmethod
+    def backward(ctx, dpooled):
+        xhat, rstd = ctx.saved_tensors
+        S, n = ctx.dims
+        dz = torch.empty_like(xhat)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(xhat.device).cuda_stream)
+        _native.check(lib.swarm_set_pool_backward(S, n, xhat.shape[1], _ptr(dpooled.contiguous()), _ptr(xhat),
+                                                  _ptr(rstd), _ptr(dz), stream), "swarm_set_pool_backward")
+        return dz, dz, None, None
 
 
 def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
@@ -499,6 +560,18 @@ class ResidualSelfAttention(nn.Module):
     def forward(self, inp: torch.Tensor, key_mask: torch.Tensor | None = None) -> torch.Tensor:
         B, N, D = inp.shape
         H, d = self.num_heads, self.head_dim
+        if self._native_core(inp) and FUSED_NORMS and key_mask is None and D in _native.NORM_WIDTHS:
+            # both LayerNorms, the residual add and the set mean on swarm_row_norm_* /
+            # swarm_set_pool_* (one pass each way instead of torch's layer_norm / add / mean)
+            x2 = _RowNorm.apply(inp.reshape(B * N, D).contiguous())
+            w = torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight])
+            b = torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias])
+            if torch.is_grad_enabled() and B * N >= SPLITK_MIN_ROWS:
+                qkv = _SplitKLinear.apply(x2, w, b)
+            else:
+                qkv = torch.nn.functional.linear(x2, w, b).contiguous()
+            att = _AttnCore.apply(qkv, None, B, N, H)
+            return _SetPool.apply(self.fc_out(att).contiguous(), x2, B, N)
         x = self.embedding_norm(inp)
         if self._native_core(inp):
             # the three projections as one GEMM (q | k | v column blocks), then the attention

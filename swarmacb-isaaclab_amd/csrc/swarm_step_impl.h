@@ -141,6 +141,15 @@
 #ifndef SWARM_WAVE_TIMING
 #define SWARM_WAVE_TIMING 0
 #endif
+// Observation pass of the production kernel (no replay, 6-7-neighbour chunks):
+// the proximity and range-and-bearing candidate masks from ONE read of the
+// part's tile entries, the packet-loss Philox block drawn before the proximity
+// loops (its multiply chain overlaps them), and the line-of-sight direction
+// divided out only when some segment is tested. Same draws, same terms, same
+// order: bitwise-neutral.
+#ifndef SWARM_OBS_FUSE
+#define SWARM_OBS_FUSE 1
+#endif
 
 namespace swarm {
 
@@ -395,6 +404,29 @@ __device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, 
         m |= c ? (1u << jj) : 0u;
     }
     return m;
+}
+
+// Both observation masks of a part's chunk from one read of its C tile entries:
+// proximity discs (|d|^2 <= 0.02) and range-and-bearing candidates
+// (|d|^2 + 1e-8 < rab_range2_hi); the same tests as the two chunk_mask calls.
+template <int C>
+__device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const float2* xy, float x, float y,
+                                          uint32_t& mprox, uint32_t& mrab) {
+    float2 p[C];
+#pragma unroll
+    for (int jj = 0; jj < C; ++jj) p[jj] = xy[L.ab + L.j0 + jj];
+    uint32_t a = 0, b = 0;
+#pragma unroll
+    for (int jj = 0; jj < C; ++jj) {
+        const int j = L.j0 + jj;
+        const bool ok = (j < L.j1) & (j != L.i);
+        const float dx = p[jj].x - x, dy = p[jj].y - y;
+        const float s = dx * dx + dy * dy;
+        a |= (ok & (s <= 0.0200f)) ? (1u << jj) : 0u;
+        b |= (ok & (s + 1e-8f < g.rab_range2_hi)) ? (1u << jj) : 0u;
+    }
+    mprox = a;
+    mrab = b;
 }
 
 // f(j, p_j) for every candidate j of this part's chunk (bits of `cand`), in
@@ -825,7 +857,8 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
 template <int LY, int C>
 __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const Shared<LY>& S, float x, float y,
-                                                  const float rdx[8], const float rdy[8], float prox[8]) {
+                                                  const float rdx[8], const float rdy[8], float prox[8],
+                                                  const uint32_t* disc_cand = nullptr) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length.
@@ -920,8 +953,9 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             if (j < L.j1 && j != L.i && dx * dx + dy * dy <= 0.0200f) disc(dx, dy);
         }
     } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
-        const uint32_t cand = chunk_mask<C>(L, S.xy, x, y,
-                                            [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
+        const uint32_t cand = disc_cand ? *disc_cand
+                                        : chunk_mask<C>(L, S.xy, x, y,
+                                                        [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
         for_each_cand(L, S.xy, cand, [&](int, float2 p) {
             SWARM_WT(L.wt_disc++);
             disc(p.x - x, p.y - y);
@@ -999,7 +1033,8 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
 template <int C>
 __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv, float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
-                                            uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy) {
+                                            uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy,
+                                            const uint32_t* pre_cand = nullptr, const uint4* pre_rb = nullptr) {
     const bool me_in = insv[L.r] != 0;
     n = 0.0f;
     wx = 0.0f;
@@ -1013,9 +1048,14 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         // line of sight (ES:462-501): arena faces can only block if an end point is
         // not strictly inside the convex arena; internal walls are always tested.
         const bool test_arena = !(me_in && insv[L.ab + j] != 0);
-        const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
+        const int s0 = test_arena ? 0 : 12;
         bool blocked = false;
-        for (int s = test_arena ? 0 : 12; s < g.nseg; ++s) {
+#if SWARM_OBS_FUSE
+        // no segment to test (convex arena only, both ends strictly inside): skip the divisions
+        if (s0 < g.nseg) {
+#endif
+        const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
+        for (int s = s0; s < g.nseg; ++s) {
             const float sx = g.seg_sx[s], sy = g.seg_sy[s];
             const float qx = g.seg_ax[s] - x, qy = g.seg_ay[s] - y;
             const float den = rdx * sy - rdy * sx;
@@ -1024,6 +1064,9 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
             const float u = (qx * rdy - qy * rdx) / dd;
             blocked |= fabsf(den) > 1e-8f && t > 1e-5f && t < dist - 1e-5f && u >= 0.0f && u <= 1.0f;
         }
+#if SWARM_OBS_FUSE
+        }
+#endif
         if (blocked) return;
         n += 1.0f;
         const float du = dist * g.inv_unity;
@@ -1078,12 +1121,13 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
     } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18) {
         // as the K18 path below: every candidate's packet-loss uniform first (one
         // Philox block per chunk), then the term for the kept neighbours in increasing j
-        const uint32_t cand = chunk_mask<C>(L, xy, x, y, [&](float dx, float dy) {
+        const uint32_t cand = pre_cand ? *pre_cand : chunk_mask<C>(L, xy, x, y, [&](float dx, float dy) {
             return dx * dx + dy * dy + 1e-8f < g.rab_range2_hi;
         });
         uint32_t kept = 0;
         if (cand) {
             const uint4 rb = u_replay ? make_uint4(0, 0, 0, 0)
+                             : pre_rb ? *pre_rb
                                       : rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), purpose, tick);
 #pragma unroll
             for (int jj = 0; jj < C; ++jj) {
@@ -1387,14 +1431,23 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     }
     float prox[8], lt[8], r4[4], zt;
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
+    constexpr bool FUSE = SWARM_OBS_FUSE && C > 0 && SWARM_BRANCHFREE_CHUNKS && !SWARM_UNROLLED_CHUNKS &&
+                          ChunkRng<C>::K18 && SWARM_ABLATE == 0;
+    uint32_t mprox = 0, mrab = 0;
+    uint4 rb = make_uint4(0, 0, 0, 0);
+    if constexpr (FUSE) {
+        obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
+        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+    }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox);
+        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr);
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
-        rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy);
+        rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
+                       FUSE ? &mrab : nullptr, FUSE ? &rb : nullptr);
     SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
