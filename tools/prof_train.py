@@ -49,12 +49,15 @@ def main():
         torch.cuda.synchronize()
         return
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
         tr.update()
         torch.cuda.synchronize()
     ka = prof.key_averages()
-    print(ka.table(sort_by="cuda_time_total", row_limit=40))
-    print(ka.table(sort_by="cpu_time_total", row_limit=25))
+    print(ka.table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=150))
+    # the aten ops behind them, by input shape
+    ks = prof.key_averages(group_by_input_shape=True)
+    print(ks.table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=40,
+                   max_shapes_column_width=110))
     n_kernels = sum(e.count for e in ka if e.device_type == torch.autograd.DeviceType.CUDA)
     print(f"device kernels per optimizer step: {n_kernels / a.steps:.0f}")
 
