@@ -125,6 +125,16 @@ int32_t swarm_set_pool_forward(int64_t sets, int32_t n, int32_t width, const flo
 int32_t swarm_set_pool_backward(int64_t sets, int32_t n, int32_t width, const float* dpooled, const float* xhat,
                                 const float* rstd, float* dz, void* stream);
 
+/* Reductions of the split-row weight gradient of the critic's entity-row layers (agents/poca_networks.py
+ * _SplitKLinear: dW = dy^T x over R = 40-164 k rows as c partial products of 1024-row chunks).
+ * swarm_splitk_colsum: partials[s][j] = sum of dy[r][j] over the rows r of slab s (rows [s*slab, (s+1)*slab)),
+ *   dy: [rows][out] (out % 4 == 0, out <= 1024, 16-byte aligned).
+ * swarm_splitk_finish: dw[e] = sum_{k < chunks} pw[k][e] (e < n_w) and db[j] = sum_{s < slabs} pb[s][j]
+ *   (j < n_b; n_b = 0: no bias), each summed in a fixed order (deterministic). */
+int32_t swarm_splitk_colsum(int64_t rows, int32_t out, int32_t slab, const float* dy, float* partials, void* stream);
+int32_t swarm_splitk_finish(int32_t chunks, int64_t n_w, const float* pw, float* dw, int32_t slabs, int32_t n_b,
+                            const float* pb, float* db, void* stream);
+
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
  * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.

@@ -72,7 +72,8 @@ CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
                  "swarm_rsa_attn_backward", "swarm_tensor_list_copy", "swarm_lstm_seq_forward_batch",
                  "swarm_lstm_seq_backward_batch", "swarm_row_norm_forward", "swarm_row_norm_backward",
-                 "swarm_set_pool_forward", "swarm_set_pool_backward"]
+                 "swarm_set_pool_forward", "swarm_set_pool_backward", "swarm_splitk_colsum",
+                 "swarm_splitk_finish"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 
@@ -184,6 +185,10 @@ def load() -> C.CDLL:
     lib.swarm_set_pool_forward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, vp]
     lib.swarm_set_pool_backward.restype = i32
     lib.swarm_set_pool_backward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp]
+    lib.swarm_splitk_colsum.restype = i32
+    lib.swarm_splitk_colsum.argtypes = [i64, i32, i32, vp, vp, vp]
+    lib.swarm_splitk_finish.restype = i32
+    lib.swarm_splitk_finish.argtypes = [i32, i64, vp, vp, i32, i32, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -218,22 +218,43 @@ class LearnedOptionActor(nn.Module):
         """(B, T, obs) -> selector logits, option values (B, T, O), termination logits
         (B, T, O), action means / stds (B, T, O, act), attentions (B, T, O, obs), memory
         (LON:392-514)."""
+        item, ctx = self.manager_stage(obs_seq, state)
+        item, ctx = self.option_stage(ctx, _lstm(*item))
+        return self.head_stage(ctx, _lstm(*item))
+
+    # forward_sequence in three stages around its two recurrences, so that a caller can run
+    # the LSTMs of several independent forwards (the update's actor and its frozen reference,
+    # the critics' memories) in one launch each (poca_networks.lstm_sequences)
+    def manager_stage(self, obs_seq: torch.Tensor, state=None):
+        """Up to the manager LSTM: (its item (lstm, sequence, state, keep), context)."""
         if obs_seq.ndim != 3 or obs_seq.shape[-1] != self.obs_dim:
             raise ValueError(f"Expected observations (batch, time, {self.obs_dim}), got {tuple(obs_seq.shape)}")
         B, T = obs_seq.shape[:2]
-        O, D, H = self.num_options, self.obs_dim, self.option_hidden
         if state is None:
             state = self.initial_state(B, obs_seq.device)
         manager_state, option_state = self._unpack_state(state, B)
-        manager_obs = obs_seq[..., 16:20] if D == 24 else obs_seq
+        manager_obs = obs_seq[..., 16:20] if self.obs_dim == 24 else obs_seq
         manager_enc = self.manager_encoder(manager_obs.reshape(-1, self.manager_obs_dim)).view(B, T, -1)
-        manager_features, next_manager_state = _lstm(self.manager_lstm, manager_enc, manager_state)
+        return (self.manager_lstm, manager_enc, manager_state, None), (obs_seq, option_state)
+
+    def option_stage(self, ctx, manager_out):
+        """From the manager LSTM's output to the option LSTM: (its item, context)."""
+        obs_seq, option_state = ctx
+        B, T = obs_seq.shape[:2]
+        O, D, H = self.num_options, self.obs_dim, self.option_hidden
+        manager_features, next_manager_state = manager_out
         sensor_context = self.attention_encoder(obs_seq.reshape(-1, D)).view(B, T, self.manager_hidden_size)
         attentions = torch.sigmoid(self.attention_head(manager_features + sensor_context).view(B, T, O, D))
         # every option sees only its attended observation h_omega(x) * x
         option_seq = (obs_seq.unsqueeze(-2) * attentions).permute(0, 2, 1, 3).reshape(B * O, T, D)
         option_enc = self.option_sensor_encoder(option_seq.reshape(-1, D)).view(B * O, T, H)
-        option_rec, next_option_state = _lstm(self.option_lstm, option_enc, option_state)
+        return (self.option_lstm, option_enc, option_state, None), (B, T, attentions, option_enc, next_manager_state)
+
+    def head_stage(self, ctx, option_out):
+        """From the option LSTM's output to forward_sequence's outputs."""
+        B, T, attentions, option_enc, next_manager_state = ctx
+        O, H = self.num_options, self.option_hidden
+        option_rec, next_option_state = option_out
         option_features = self.option_output_encoder(
             torch.cat([option_enc, option_rec], dim=-1).reshape(-1, H + self.option_recurrent_size)
         ).view(B, O, T, H).permute(0, 2, 1, 3)

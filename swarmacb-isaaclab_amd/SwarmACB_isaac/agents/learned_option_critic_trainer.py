@@ -44,7 +44,7 @@ from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
 from .learned_option_critic_networks import (LEARNED_OPTION_CRITIC_VERSION, LearnedOptionActor,
                                              termination_objective)
 from .option_collector import LearnedOptionCollector
-from .poca_networks import POCACritic, batched_sequence_passes
+from .poca_networks import POCACritic, batched_sequence_passes, lstm_sequences
 
 __all__ = ["LearnedOptionCriticConfig", "LearnedOptionCriticTrainer", "stable_trust_region_policy_loss"]
 
@@ -320,12 +320,45 @@ class LearnedOptionCriticTrainer(TrainerBase):
         n_term = d_term if d_term is not None else term_mask.sum().clamp_min(1)
 
         mem0 = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
-        (_sel, option_values, _term, action_means, action_stds, attentions,
-         _next) = self.actor.forward_sequence(obs, mem0)
+        # the manager LSTMs of the actor and of the frozen update-start actor share one launch,
+        # their option LSTMs the next, the three critics' memories a third (every problem of a
+        # launch is computed exactly as alone; the frozen actor takes no part in the backward;
+        # actor and critics keep separate launches: their losses are differentiated separately)
+        flat_states = states.reshape(B * L, N, self.state_dim)
+        flat_next_states = next_states.reshape_as(flat_states)
+        flat_joint_options = joint_options.reshape(B * L, N)
+        encoded = self._encode_options(flat_joint_options)
+        flat_joint_actions = joint_actions.reshape(B * L, N, A)
+        option_states = self._option_augmented_states(flat_states, flat_joint_options)
+        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
+
+        def mem(k):
+            return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
+
+        # team critic_pass, action-critic focal_baselines and the option critic's joint_action_pass +
+        # focal_baselines (one batched pass per critic)
+        critic_requests = [
+            (self.team_critic, flat_states, None, focal_ids, {"value": mem("team_memory")}, L, ("value",)),
+            (self.action_critic, option_states, flat_joint_actions, focal_ids,
+             {"baseline": mem("action_baseline_memory")}, L, ("baseline",)),
+            (self.option_critic, flat_states, encoded, focal_ids,
+             {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")}, L,
+             ("joint", "baseline"))]
+        a_item, a_ctx = self.actor.manager_stage(obs, mem0)
         with torch.no_grad():
-            ref_out = reference_actor.forward_sequence(obs, (batch["memory_h"].unsqueeze(0),
-                                                             batch["memory_c"].unsqueeze(0)))
+            r_item, r_ctx = reference_actor.manager_stage(obs, (batch["memory_h"].unsqueeze(0),
+                                                                batch["memory_c"].unsqueeze(0)))
+        outs = lstm_sequences([a_item, r_item + (True,)])
+        a_item, a_ctx = self.actor.option_stage(a_ctx, outs[0])
+        with torch.no_grad():
+            r_item, r_ctx = reference_actor.option_stage(r_ctx, outs[1])
+        opt_outs = lstm_sequences([a_item, r_item + (True,)])
+        (_sel, option_values, _term, action_means, action_stds, attentions,
+         _next) = self.actor.head_stage(a_ctx, opt_outs[0])
+        with torch.no_grad():
+            ref_out = reference_actor.head_stage(r_ctx, opt_outs[1])
             ref_means, ref_stds = ref_out[3], ref_out[4]
+        ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes(critic_requests)
 
         # AOC: the manager is epsilon-soft over Q_Omega; no selector gradient (LOT:1050-1093)
         option_dist = self.actor.option_dist(option_values, epsilon=self.current_option_epsilon)
@@ -364,32 +397,12 @@ class LearnedOptionCriticTrainer(TrainerBase):
         next_beta_logits = self.actor.selected_termination_logits(next_term_logits, options.reshape(-1)).view(B, L)
         next_beta = torch.sigmoid(next_beta_logits)
 
-        flat_states = states.reshape(B * L, N, self.state_dim)
-        flat_next_states = next_states.reshape_as(flat_states)
-        flat_joint_options = joint_options.reshape(B * L, N)
-        encoded = self._encode_options(flat_joint_options)
-        flat_joint_actions = joint_actions.reshape(B * L, N, A)
-        option_states = self._option_augmented_states(flat_states, flat_joint_options)
-        focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
         flat_returns = batch["returns"].reshape(-1)
         flat_mask = loss_mask.reshape(-1)
         selected_local = option_values.gather(-1, options.unsqueeze(-1)).squeeze(-1).reshape(-1)
         local_option_value_mean = (selected_local * flat_mask).sum() / (
             n_mask_f if d_mask is not None else flat_mask.sum().clamp_min(1.0))
         option_value_spread = (option_values.std(dim=-1, unbiased=False) * loss_mask).sum() / n_mask
-
-        def mem(k):
-            return (batch[f"{k}_h"].unsqueeze(0).detach(), batch[f"{k}_c"].unsqueeze(0).detach())
-
-        # team critic_pass, action-critic focal_baselines and the option critic's joint_action_pass +
-        # focal_baselines (one batched pass): the three critics' memories in ONE LSTM launch
-        ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes([
-            (self.team_critic, flat_states, None, focal_ids, {"value": mem("team_memory")}, L, ("value",)),
-            (self.action_critic, option_states, flat_joint_actions, focal_ids,
-             {"baseline": mem("action_baseline_memory")}, L, ("baseline",)),
-            (self.option_critic, flat_states, encoded, focal_ids,
-             {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")}, L,
-             ("joint", "baseline"))])
 
         def tr_loss(new, old_key):
             return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,

@@ -17,6 +17,7 @@ it restates the reference math operation by operation.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 import os
@@ -38,6 +39,9 @@ _KERNEL_INITS = {
 
 SPLITK_MIN_ROWS = 8192     # rows from which a layer's weight gradient is split over row chunks
 SPLITK_CHUNK_ROWS = 1024   # rows per chunk of that split
+SPLITK_SLAB_ROWS = 256     # rows per column-sum slab of its bias gradient
+# False (or SWARM_SPLITK_SUMS=0): the chunk / bias sums run torch's reductions
+SPLITK_NATIVE_SUMS = os.environ.get("SWARM_SPLITK_SUMS", "1") != "0"
 
 
 class _SplitKLinear(torch.autograd.Function):
@@ -62,8 +66,30 @@ class _SplitKLinear(torch.autograd.Function):
         c = R // SPLITK_CHUNK_ROWS
         L = R // c
         main = c * L
-        dyc = dy[:main].view(c, L, dy.shape[1])
-        dw = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1])).sum(dim=0)
+        out_f = dy.shape[1]
+        dyc = dy[:main].view(c, L, out_f)
+        parts = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1]))
+        if SPLITK_NATIVE_SUMS and dy.is_cuda and out_f % 4 == 0 and out_f <= 1024:
+            # the chunk sum of the partial products and the bias gradient (column sums of dy
+            # per slab, then over the slabs) in two launches (swarm_splitk_colsum / _finish)
+            dy = dy.contiguous()
+            lib = _native.load()
+            stream = C.c_void_p(torch.cuda.current_stream(dy.device).cuda_stream)
+            dw = torch.empty(out_f, x.shape[1], dtype=dy.dtype, device=dy.device)
+            db, pb, slabs = None, None, 0
+            if ctx.has_bias:
+                slabs = (R + SPLITK_SLAB_ROWS - 1) // SPLITK_SLAB_ROWS
+                pb = torch.empty(slabs, out_f, dtype=dy.dtype, device=dy.device)
+                db = torch.empty(out_f, dtype=dy.dtype, device=dy.device)
+                _native.check(lib.swarm_splitk_colsum(R, out_f, SPLITK_SLAB_ROWS, _ptr(dy), _ptr(pb), stream),
+                              "swarm_splitk_colsum")
+            _native.check(lib.swarm_splitk_finish(c, dw.numel(), _ptr(parts), _ptr(dw), slabs,
+                                                  out_f if ctx.has_bias else 0, _ptr(pb), _ptr(db), stream),
+                          "swarm_splitk_finish")
+            if main < R:
+                dw.addmm_(dy[main:].t(), x[main:])
+            return dx, dw, db
+        dw = parts.sum(dim=0)
         db = dyc.sum(dim=1).sum(dim=0) if ctx.has_bias else None
         if main < R:
             dw.addmm_(dy[main:].t(), x[main:])
@@ -173,8 +199,13 @@ class _LSTMSequences(torch.autograd.Function):
     def backward(ctx, *grads):
         k = ctx.k
         saved = ctx.saved_tensors
-        descs, res, keepalive = [], [], []
-        for i in range(k):
+        # problems none of whose inputs need a gradient (a frozen network's forward run in the
+        # same launch) take no part in the backward launch
+        live = [i for i in range(k) if any(ctx.needs_input_grad[1 + 5 * i:1 + 5 * i + 4])]
+        if not live:
+            return (None,) * (1 + 5 * k)
+        descs, res, keepalive = [], {}, []
+        for i in live:
             w_hh, h0, c0, keep, h_out, c_out, act = saved[7 * i:7 * i + 7]
             dh_out, dc_n = grads[2 * i].contiguous(), grads[2 * i + 1].contiguous()
             dxg = torch.empty_like(act)
@@ -183,15 +214,18 @@ class _LSTMSequences(torch.autograd.Function):
                                             _addr(act), _addr(dh_out), None, _addr(dc_n), _addr(dxg), _addr(dh0),
                                             _addr(dc0)))
             keepalive += [dh_out, dc_n]
-            res.append((dxg, dh0, dc0))
+            res[i] = (dxg, dh0, dc0)
         n0, T, U = saved[4].shape
-        arr = (_native.LstmSeqBwd * k)(*descs)
+        arr = (_native.LstmSeqBwd * len(live))(*descs)
         lib = _native.load()
         stream = C.c_void_p(torch.cuda.current_stream(saved[4].device).cuda_stream)
-        _native.check(lib.swarm_lstm_seq_backward_batch(k, T, U, C.cast(arr, C.c_void_p), stream),
+        _native.check(lib.swarm_lstm_seq_backward_batch(len(live), T, U, C.cast(arr, C.c_void_p), stream),
                       "swarm_lstm_seq_backward_batch")
         out = [None]
         for i in range(k):
+            if i not in res:
+                out += [None] * 5
+                continue
             w_hh, h0, c0, keep, h_out, c_out, act = saved[7 * i:7 * i + 7]
             dxg, dh0, dc0 = res[i]
             dw = None
@@ -316,27 +350,39 @@ def lstm_sequences(items):
     """[lstm_sequence(lstm, seq, state, keep) for each item] with the GPU recurrences of items
     that share a sequence length and unit count in ONE launch each way (_LSTMSequences): the
     actor's and the critics' memories of a minibatch are independent, and one launch runs
-    their latency-bound chains side by side instead of back to back."""
+    their latency-bound chains side by side instead of back to back. An item may carry a fifth
+    element `frozen` = True: its forward runs without autograd (as under torch.no_grad, its
+    outputs detached) and it takes no part in the backward launch."""
     out = [None] * len(items)
     groups: dict = {}
-    for i, (lstm, seq, state, keep) in enumerate(items):
+    for i, item in enumerate(items):
+        lstm, seq, state, keep = item[:4]
         if _fused_seq_ok(lstm, seq):
             groups.setdefault((seq.shape[1], lstm.hidden_size, seq.device), []).append(i)
         else:
-            out[i] = _lstm_loop(lstm, seq, state, keep)
+            frozen = len(item) > 4 and item[4]
+            with torch.no_grad() if frozen else contextlib.nullcontext():
+                out[i] = _lstm_loop(lstm, seq, state, keep)
     for idx in groups.values():
         for chunk in (idx[j:j + _native.LSTM_MAX_BATCH] for j in range(0, len(idx), _native.LSTM_MAX_BATCH)):
-            args = []
+            args, frozen_of = [], []
             for i in chunk:
-                lstm, seq, state, keep = items[i]
+                lstm, seq, state, keep = items[i][:4]
+                frozen = len(items[i]) > 4 and items[i][4]
                 n, units = seq.shape[0], lstm.hidden_size
-                xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
-                args += [xg.contiguous(), lstm.weight_hh_l0.contiguous(), state[0].reshape(n, units).contiguous(),
-                         state[1].reshape(n, units).contiguous(),
-                         keep.to(torch.float32).contiguous() if keep is not None else None]
+                with torch.no_grad() if frozen else contextlib.nullcontext():
+                    xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
+                    w_hh = lstm.weight_hh_l0.contiguous()
+                    h0, c0 = state[0].reshape(n, units).contiguous(), state[1].reshape(n, units).contiguous()
+                if frozen:
+                    xg, w_hh, h0, c0 = xg.detach(), w_hh.detach(), h0.detach(), c0.detach()
+                args += [xg.contiguous(), w_hh, h0, c0, keep.to(torch.float32).contiguous() if keep is not None else None]
+                frozen_of.append(frozen)
             res = _LSTMSequences.apply(len(chunk), *args)
             for j, i in enumerate(chunk):
                 h_seq, c_n = res[2 * j], res[2 * j + 1]
+                if frozen_of[j]:
+                    h_seq, c_n = h_seq.detach(), c_n.detach()
                 out[i] = (h_seq, (h_seq[:, -1].unsqueeze(0), c_n.unsqueeze(0)))
     return out
 

@@ -47,6 +47,12 @@
 #ifndef RSA_GEMM_SCHED_BARRIER
 #define RSA_GEMM_SCHED_BARRIER 1
 #endif
+// 1: rsa_baselines_kernel issues a head's projected-value MFMAs, then runs that head's softmax
+// on the VALU while they are in flight, and only then stores their results (the two are
+// independent); 0: projected values stored first, softmax after.
+#ifndef RSA_VW_OVERLAP
+#define RSA_VW_OVERLAP 1
+#endif
 
 namespace {
 
@@ -489,8 +495,37 @@ __global__ void __launch_bounds__(NT) rsa_baselines_kernel(int B, const float* _
 #pragma unroll
             for (int ks = 0; ks < DH / 4; ++ks) wb[ks] = Wo[col * HD + h * DH + (DH / 4) * kq + ks];
             // VW_h[row][col] for the 2N rows (3 row tiles, rows >= 2N dropped)
+            constexpr int RT = (RSA_ABLATE & 8) ? 0 : (R + 15) / 16;
+#if RSA_VW_OVERLAP
+            // the three row tiles' MFMA chains first (their A operands read from LDS up front),
+            // then this head's softmax on the VALU while the matrix cores work, then the stores
+            f32x4 vacc[RT > 0 ? RT : 1];
 #pragma unroll
-            for (int rt = 0; rt < ((RSA_ABLATE & 8) ? 0 : (R + 15) / 16); ++rt) {
+            for (int rt = 0; rt < RT; ++rt) vacc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int m = 0; m < DH / 4; m += 4) {
+#pragma unroll
+                for (int rt = 0; rt < RT; ++rt) {
+                    const float4 v = *reinterpret_cast<const float4*>(
+                        &Vs[min(16 * rt + cl, R - 1) * LDSW + h * DH + (DH / 4) * kq + m]);
+                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, wb[m + 0], vacc[rt], 0, 0, 0);
+                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, wb[m + 1], vacc[rt], 0, 0, 0);
+                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, wb[m + 2], vacc[rt], 0, 0, 0);
+                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, wb[m + 3], vacc[rt], 0, 0, 0);
+                }
+            }
+            softmax(h);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = 16 * rt + 4 * kq + i;
+                    if (r < R) VW[r * LDSW + col] = vacc[rt][i];
+                }
+            }
+#else
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt) {
                 const float* vp = &Vs[min(16 * rt + cl, R - 1) * LDSW + h * DH + (DH / 4) * kq];
                 f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -510,6 +545,7 @@ __global__ void __launch_bounds__(NT) rsa_baselines_kernel(int B, const float* _
                 __builtin_amdgcn_sched_barrier(0);
             }
             softmax(h);
+#endif
             __syncthreads();
             // acc[t] += P[rows of tile t][action j] VW_h[N + j][col]; k-step m of lane group kq
             // is action j = (N/4) kq + m

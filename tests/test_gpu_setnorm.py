@@ -1,4 +1,4 @@
-"""The LayerNorm kernels of ResidualSelfAttention's training path (swarm_row_norm_* /
+"""The LayerNorm and split-row gradient kernels of the critic's training path (swarm_row_norm_* /
 swarm_set_pool_*, include/swarmtrain.h) against torch's layer_norm / add / mean in fp32
 (the reference's formulation, poca_networks.py:417-491), forward and every gradient.
 
@@ -98,3 +98,25 @@ def test_norm_kernels_refuse_bad_arguments(gpu_device):
                                       x.data_ptr(), None) != 0
     assert lib.swarm_row_norm_backward(4, 128, x.data_ptr() + 4, x.data_ptr(), r.data_ptr(), x.data_ptr(),
                                        None) != 0
+
+
+@pytest.mark.parametrize("rows,fin,fout,bias", [(40960, 5, 128, True), (81920, 128, 384, True),
+                                                 (9000, 11, 128, True), (16384, 128, 128, False)])
+def test_splitk_linear_gradients(rows, fin, fout, bias, gpu_device):
+    """_SplitKLinear's weight / bias gradients through swarm_splitk_colsum / _finish against
+    torch's linear backward (fp32 sums in another order: 2e-5 of scale)."""
+    from SwarmACB_isaac.agents.poca_networks import _SplitKLinear
+
+    g = torch.Generator(device=gpu_device).manual_seed(rows + fout)
+    x = torch.randn(rows, fin, device=gpu_device, generator=g)
+    w0 = torch.randn(fout, fin, device=gpu_device, generator=g) * 0.1
+    b0 = torch.randn(fout, device=gpu_device, generator=g) if bias else None
+    dy = torch.randn(rows, fout, device=gpu_device, generator=g)
+    w1, w2 = w0.clone().requires_grad_(True), w0.clone().requires_grad_(True)
+    b1 = b0.clone().requires_grad_(True) if bias else None
+    b2 = b0.clone().requires_grad_(True) if bias else None
+    _SplitKLinear.apply(x, w1, b1).backward(dy)
+    F.linear(x, w2, b2).backward(dy)
+    _close(w1.grad, w2.grad, 2e-5, "dW")
+    if bias:
+        _close(b1.grad, b2.grad, 2e-5, "db")

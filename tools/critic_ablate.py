@@ -19,6 +19,7 @@ bo = torch.randn(h, device=dev)
 out = torch.empty(E * N, h, device=dev)
 p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 res = {}
+first = None
 for path in sorted(glob.glob(os.path.join(ROOT, "build/ablate/libcritic_*.so"))):
     lib = C.CDLL(path)
     lib.swarm_rsa_pool.argtypes = [C.c_int32] * 5 + [C.c_void_p] * 6
@@ -32,5 +33,10 @@ for path in sorted(glob.glob(os.path.join(ROOT, "build/ablate/libcritic_*.so")))
         run()
     b.record()
     torch.cuda.synchronize()
-    res[os.path.basename(path)] = a.elapsed_time(b) / 10
+    ms = a.elapsed_time(b) / 10
+    # every variant against the first one's output (ablation variants differ by design)
+    diff = 0.0 if first is None else float((out - first).abs().max())
+    if first is None:
+        first = out.clone()
+    res[os.path.basename(path)] = {"ms": ms, "max_abs_diff_vs_first": diff}
 print(json.dumps(res, indent=1))
