@@ -49,9 +49,12 @@
 #endif
 // 1: rsa_baselines_kernel issues a head's projected-value MFMAs, then runs that head's softmax
 // on the VALU while they are in flight, and only then stores their results (the two are
-// independent); 0: projected values stored first, softmax after.
+// independent); 0: projected values stored first, softmax after. Measured at C3 (8192 envs,
+// tools/critic_ablate.py, identical outputs): 1.58 ms with the overlap vs 1.48 ms without (the
+// three live accumulator chains and the softmax's registers serialise worse than the stores),
+// so 0 is the default.
 #ifndef RSA_VW_OVERLAP
-#define RSA_VW_OVERLAP 1
+#define RSA_VW_OVERLAP 0
 #endif
 
 namespace {
