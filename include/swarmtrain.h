@@ -135,6 +135,33 @@ int32_t swarm_splitk_colsum(int64_t rows, int32_t out, int32_t slab, const float
 int32_t swarm_splitk_finish(int32_t chunks, int64_t n_w, const float* pw, float* dw, int32_t slabs, int32_t n_b,
                             const float* pb, float* db, void* stream);
 
+/* The PPO trust-region loss terms of every trainer (ML-Agents trust_region_value_loss /
+ * trust_region_policy_loss, reference agents/poca_trainer.py:144-191; the log-ratio-bounded policy loss
+ * of learned_option_critic_trainer.py:45-72 with stable = 1) as masked means over M rows:
+ *   value:  l = max((ret - v)^2, (ret - (old + clamp(v - old, -eps, eps)))^2)
+ *   policy: r = exp(logp - old) (log-ratio clamped to +-20 when stable), l = -min(r adv, clamp(r, lo, hi) adv)
+ *           over M rows x A columns, adv per row (adv_cols = 1) or per element (adv_cols = A);
+ *           lo / hi = 1 -+ eps rounded from double
+ *   loss = sum(l * active) / (*denom if denom else max(sum(active), 1)), active = mask_f32 or mask_u8 (at
+ *          most one; neither: every row active and the denominator is the element count)
+ * Forward writes *loss and the denominator it used (*used_denom, read by the backward); the backward reads
+ * the incoming gradient from *grad (device scalar) and writes d_values / d_log_probs for every element,
+ * with torch's subgradients (clamp passes on the closed interval, max / min split ties in half). */
+int32_t swarm_ppo_value_loss(int64_t M, const float* values, const float* old_values, const float* returns,
+                             const float* mask_f32, const uint8_t* mask_u8, float epsilon, const float* denom,
+                             float* loss, float* used_denom, void* stream);
+int32_t swarm_ppo_value_loss_backward(int64_t M, const float* values, const float* old_values, const float* returns,
+                                      const float* mask_f32, const uint8_t* mask_u8, float epsilon,
+                                      const float* used_denom, const float* grad, float* d_values, void* stream);
+int32_t swarm_ppo_policy_loss(int64_t M, int32_t A, int32_t adv_cols, const float* advantages, const float* log_probs,
+                              const float* old_log_probs, const float* mask_f32, const uint8_t* mask_u8,
+                              float clip_lo, float clip_hi, int32_t stable, const float* denom, float* loss,
+                              float* used_denom, void* stream);
+int32_t swarm_ppo_policy_loss_backward(int64_t M, int32_t A, int32_t adv_cols, const float* advantages,
+                                       const float* log_probs, const float* old_log_probs, const float* mask_f32,
+                                       const uint8_t* mask_u8, float clip_lo, float clip_hi, int32_t stable,
+                                       const float* used_denom, const float* grad, float* d_log_probs, void* stream);
+
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
  * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.

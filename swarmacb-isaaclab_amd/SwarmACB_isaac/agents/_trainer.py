@@ -10,12 +10,15 @@ on top of the multi-GPU collectives of agents/distributed.py.
 
 from __future__ import annotations
 
+import ctypes as C
 import itertools
+import os
 import time
 from pathlib import Path
 
 import torch
 
+from .. import _native
 from .distributed import TrainerComm
 from . import _graph
 from .metrics import make_writer
@@ -46,8 +49,138 @@ def masked_mean(loss, mask, denom=None):
     return loss.sum() / denom if denom is not None else loss.mean()
 
 
+# False (or SWARM_FUSED_LOSSES=0): the PPO loss terms run torch's elementwise ops (the reference's)
+FUSED_LOSSES = os.environ.get("SWARM_FUSED_LOSSES", "1") != "0"
+
+
+def _vp(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _loss_mask(mask, rows: int):
+    """(f32 mask, u8 mask) views for swarm_ppo_*_loss, or None if the mask does not fit."""
+    if mask is None:
+        return None, None
+    if mask.dim() != 1 or mask.numel() != rows or mask.device.type != "cuda":
+        return None
+    if mask.dtype == torch.bool:
+        return None, mask.contiguous().view(torch.uint8)
+    if mask.dtype == torch.float32:
+        return mask.contiguous(), None
+    return mask.to(torch.float32).contiguous(), None
+
+
+def _loss_denom(denom, device):
+    if denom is None:
+        return None
+    if not (torch.is_tensor(denom) and denom.numel() == 1 and denom.dtype == torch.float32
+            and denom.device == device):
+        return False
+    return denom.reshape(()).contiguous()
+
+
+class _ValueLoss(torch.autograd.Function):
+    """trust_region_value_loss on swarm_ppo_value_loss / _backward (include/swarmtrain.h): one
+    kernel each way; values, old values and returns flattened to M rows."""
+
+    @staticmethod
+    def forward(ctx, values, old_values, returns, mask_f, mask_u, denom, epsilon: float):
+        v = values.reshape(-1).contiguous()
+        o, r = old_values.reshape(-1).contiguous(), returns.reshape(-1).contiguous()
+        loss = torch.empty((), dtype=v.dtype, device=v.device)
+        used = torch.empty((), dtype=v.dtype, device=v.device)
+        stream = C.c_void_p(torch.cuda.current_stream(v.device).cuda_stream)
+        _native.check(_native.load().swarm_ppo_value_loss(v.numel(), _vp(v), _vp(o), _vp(r), _vp(mask_f), _vp(mask_u),
+                                                          epsilon, _vp(denom), _vp(loss), _vp(used), stream),
+                      "swarm_ppo_value_loss")
+        ctx.save_for_backward(v, o, r, mask_f, mask_u, used)
+        ctx.epsilon, ctx.shape = epsilon, values.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        v, o, r, mask_f, mask_u, used = ctx.saved_tensors
+        dv = torch.empty_like(v)
+        stream = C.c_void_p(torch.cuda.current_stream(v.device).cuda_stream)
+        _native.check(_native.load().swarm_ppo_value_loss_backward(
+            v.numel(), _vp(v), _vp(o), _vp(r), _vp(mask_f), _vp(mask_u), ctx.epsilon, _vp(used),
+            _vp(g.reshape(()).contiguous()), _vp(dv), stream), "swarm_ppo_value_loss_backward")
+        return dv.view(ctx.shape), None, None, None, None, None, None
+
+
+class _PolicyLoss(torch.autograd.Function):
+    """trust_region_policy_loss (stable = the log-ratio-bounded OC2 form) on swarm_ppo_policy_loss /
+    _backward: log_probs (M, A), advantages per row or per element."""
+
+    @staticmethod
+    def forward(ctx, log_probs, old_log_probs, advantages, mask_f, mask_u, denom, lo: float, hi: float,
+                stable: bool):
+        M, A = log_probs.shape
+        lp, ol = log_probs.contiguous(), old_log_probs.contiguous()
+        adv = advantages.contiguous()
+        adv_cols = 1 if adv.numel() == M else A
+        loss = torch.empty((), dtype=lp.dtype, device=lp.device)
+        used = torch.empty((), dtype=lp.dtype, device=lp.device)
+        stream = C.c_void_p(torch.cuda.current_stream(lp.device).cuda_stream)
+        _native.check(_native.load().swarm_ppo_policy_loss(M, A, adv_cols, _vp(adv), _vp(lp), _vp(ol), _vp(mask_f),
+                                                           _vp(mask_u), lo, hi, int(stable), _vp(denom), _vp(loss),
+                                                           _vp(used), stream), "swarm_ppo_policy_loss")
+        ctx.save_for_backward(lp, ol, adv, mask_f, mask_u, used)
+        ctx.args = (M, A, adv_cols, lo, hi, int(stable))
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lp, ol, adv, mask_f, mask_u, used = ctx.saved_tensors
+        M, A, adv_cols, lo, hi, stable = ctx.args
+        dlp = torch.empty_like(lp)
+        stream = C.c_void_p(torch.cuda.current_stream(lp.device).cuda_stream)
+        _native.check(_native.load().swarm_ppo_policy_loss_backward(
+            M, A, adv_cols, _vp(adv), _vp(lp), _vp(ol), _vp(mask_f), _vp(mask_u), lo, hi, stable, _vp(used),
+            _vp(g.reshape(()).contiguous()), _vp(dlp), stream), "swarm_ppo_policy_loss_backward")
+        return dlp, None, None, None, None, None, None, None, None
+
+
+def _fused_value_loss(values, old_values, returns, epsilon, mask, denom):
+    """_ValueLoss when the arguments fit it, else None (the caller runs torch's ops)."""
+    if not (FUSED_LOSSES and values.is_cuda and values.dtype == torch.float32 and old_values.dtype == torch.float32
+            and returns.dtype == torch.float32 and values.numel() > 0
+            and old_values.numel() == values.numel() == returns.numel()
+            and old_values.shape == values.shape == returns.shape
+            and not old_values.requires_grad and not returns.requires_grad):
+        return None
+    if mask is not None and values.dim() != 1:
+        return None                                     # masked_mean's broadcast of the mask
+    m = _loss_mask(mask, values.numel())
+    d = _loss_denom(denom, values.device)
+    if m is None or d is False:
+        return None
+    return _ValueLoss.apply(values, old_values, returns, m[0], m[1], d, float(epsilon))
+
+
+def _fused_policy_loss(advantages, log_probs, old_log_probs, epsilon, mask, denom, stable):
+    if not (FUSED_LOSSES and log_probs.is_cuda and log_probs.dtype == torch.float32 and log_probs.dim() == 2
+            and old_log_probs.shape == log_probs.shape and old_log_probs.dtype == torch.float32
+            and advantages.dtype == torch.float32 and not advantages.requires_grad
+            and not old_log_probs.requires_grad and log_probs.numel() > 0):
+        return None
+    M, A = log_probs.shape
+    if tuple(advantages.shape) not in ((M, 1), (M, A)):
+        return None
+    m = _loss_mask(mask, M)
+    d = _loss_denom(denom, log_probs.device)
+    if m is None or d is False:
+        return None
+    return _PolicyLoss.apply(log_probs, old_log_probs, advantages, m[0], m[1], d, 1.0 - epsilon, 1.0 + epsilon,
+                             stable)
+
+
 def trust_region_value_loss(values, old_values, returns, epsilon: float, mask=None, denom=None):
-    """ML-Agents trust_region_value_loss (poca_trainer.py:144-162)."""
+    """ML-Agents trust_region_value_loss (poca_trainer.py:144-162); on the GPU one kernel each
+    way (_ValueLoss)."""
+    fused = _fused_value_loss(values, old_values, returns, epsilon, mask, denom)
+    if fused is not None:
+        return fused
     clipped = old_values + (values - old_values).clamp(-epsilon, epsilon)
     loss = torch.max((returns - values) ** 2, (returns - clipped) ** 2)
     return masked_mean(loss, mask, denom)
@@ -55,7 +188,10 @@ def trust_region_value_loss(values, old_values, returns, epsilon: float, mask=No
 
 def trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilon: float, mask=None, denom=None):
     """ML-Agents trust_region_policy_loss, ratio clipped per action dimension
-    (poca_trainer.py:165-191)."""
+    (poca_trainer.py:165-191); on the GPU one kernel each way (_PolicyLoss)."""
+    fused = _fused_policy_loss(advantages, log_probs, old_log_probs, epsilon, mask, denom, False)
+    if fused is not None:
+        return fused
     r_theta = (log_probs - old_log_probs).exp()
     loss = -torch.min(r_theta * advantages, r_theta.clamp(1.0 - epsilon, 1.0 + epsilon) * advantages)
     return masked_mean(loss, mask, denom)

@@ -37,7 +37,7 @@ import torch.optim as optim
 from torch.distributions import Bernoulli
 
 from .. import _native
-from ._trainer import PolynomialDecay, TrainerBase, stack_obs, trust_region_value_loss
+from ._trainer import PolynomialDecay, TrainerBase, _fused_policy_loss, stack_obs, trust_region_value_loss
 from .config import PAPER_PARITY_VERSION, LearnedOptionCriticConfig
 from .distributed import TrainerComm
 from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
@@ -65,7 +65,11 @@ _COLLECTOR_STATE = LearnedOptionCollector.MEMORIES + ("current_options",)
 
 
 def stable_trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilon: float, mask=None, denom=None):
-    """PPO policy loss with the log-ratio bounded to [-20, 20] before exp (LOT:45-72)."""
+    """PPO policy loss with the log-ratio bounded to [-20, 20] before exp (LOT:45-72); on the GPU
+    one kernel each way (_trainer._PolicyLoss, stable)."""
+    fused = _fused_policy_loss(advantages, log_probs, old_log_probs, epsilon, mask, denom, True)
+    if fused is not None:
+        return fused
     ratio = (log_probs - old_log_probs).clamp(-20.0, 20.0).exp()
     loss = -torch.minimum(ratio * advantages, ratio.clamp(1.0 - epsilon, 1.0 + epsilon) * advantages)
     if mask is None:
