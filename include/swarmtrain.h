@@ -162,6 +162,20 @@ int32_t swarm_ppo_policy_loss_backward(int64_t M, int32_t A, int32_t adv_cols, c
                                        const uint8_t* mask_u8, float clip_lo, float clip_hi, int32_t stable,
                                        const float* used_denom, const float* grad, float* d_log_probs, void* stream);
 
+/* The categorical policy terms of the POCA / fixed-option OC updates (torch.distributions.Categorical over
+ * a minibatch's logits: agents/poca_trainer.py:706-745, option_critic_trainer.py:515-525): for M rows of K
+ * logits (K <= 64) and the taken actions (int64), log_probs[m] = z[m][a_m] - logsumexp(z[m]) and
+ * *mean_entropy = sum_m H_m active_m / (*denom if denom else max(sum active, 1)), H = -sum_k p_k log p_k,
+ * active = mask_u8 (NULL: all rows, denominator M). *used_denom is the denominator used (for the backward).
+ * The backward writes d_logits = g_log_probs[m] (onehot(a_m) - p) + *g_mean_entropy active_m / denom
+ * (-p (log p + H)); either gradient pointer may be NULL (= 0). */
+int32_t swarm_categorical_terms(int64_t M, int32_t K, const float* logits, const int64_t* actions,
+                                const uint8_t* mask_u8, const float* denom, float* log_probs, float* mean_entropy,
+                                float* used_denom, void* stream);
+int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logits, const int64_t* actions,
+                                         const uint8_t* mask_u8, const float* used_denom, const float* g_log_probs,
+                                         const float* g_mean_entropy, float* d_logits, void* stream);
+
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
  * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.

@@ -74,7 +74,8 @@ TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa
                  "swarm_lstm_seq_backward_batch", "swarm_row_norm_forward", "swarm_row_norm_backward",
                  "swarm_set_pool_forward", "swarm_set_pool_backward", "swarm_splitk_colsum",
                  "swarm_splitk_finish", "swarm_ppo_value_loss", "swarm_ppo_value_loss_backward",
-                 "swarm_ppo_policy_loss", "swarm_ppo_policy_loss_backward"]
+                 "swarm_ppo_policy_loss", "swarm_ppo_policy_loss_backward", "swarm_categorical_terms",
+                 "swarm_categorical_terms_backward"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 
@@ -199,6 +200,10 @@ def load() -> C.CDLL:
     lib.swarm_ppo_policy_loss.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp]
     lib.swarm_ppo_policy_loss_backward.restype = i32
     lib.swarm_ppo_policy_loss_backward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp]
+    lib.swarm_categorical_terms.restype = i32
+    lib.swarm_categorical_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.swarm_categorical_terms_backward.restype = i32
+    lib.swarm_categorical_terms_backward.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

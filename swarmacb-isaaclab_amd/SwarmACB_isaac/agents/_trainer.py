@@ -175,6 +175,58 @@ def _fused_policy_loss(advantages, log_probs, old_log_probs, epsilon, mask, deno
                              stable)
 
 
+class _CategoricalTerms(torch.autograd.Function):
+    """log_prob(actions) and the masked mean entropy of Categorical(logits) on
+    swarm_categorical_terms / _backward: logits (M, K) -> (log_probs (M,), mean entropy)."""
+
+    @staticmethod
+    def forward(ctx, logits, actions, mask_u, denom):
+        z = logits.contiguous()
+        M, K = z.shape
+        lp = torch.empty(M, dtype=z.dtype, device=z.device)
+        ent = torch.empty((), dtype=z.dtype, device=z.device)
+        used = torch.empty((), dtype=z.dtype, device=z.device)
+        stream = C.c_void_p(torch.cuda.current_stream(z.device).cuda_stream)
+        _native.check(_native.load().swarm_categorical_terms(M, K, _vp(z), _vp(actions), _vp(mask_u), _vp(denom),
+                                                             _vp(lp), _vp(ent), _vp(used), stream),
+                      "swarm_categorical_terms")
+        ctx.save_for_backward(z, actions, mask_u, used)
+        return lp, ent
+
+    @staticmethod
+    def backward(ctx, g_lp, g_ent):
+        z, actions, mask_u, used = ctx.saved_tensors
+        M, K = z.shape
+        dz = torch.empty_like(z)
+        stream = C.c_void_p(torch.cuda.current_stream(z.device).cuda_stream)
+        _native.check(_native.load().swarm_categorical_terms_backward(
+            M, K, _vp(z), _vp(actions), _vp(mask_u), _vp(used),
+            _vp(g_lp.contiguous()) if g_lp is not None else None,
+            _vp(g_ent.reshape(()).contiguous()) if g_ent is not None else None, _vp(dz), stream),
+            "swarm_categorical_terms_backward")
+        return dz, None, None, None
+
+
+def categorical_terms(logits, actions, mask=None, denom=None):
+    """(log_prob of `actions`, masked mean entropy) of Categorical(logits) over the rows of
+    logits (M, K): torch.distributions.Categorical's log_prob / entropy and the trainers'
+    (entropy * mask).sum() / (denom or mask.sum().clamp_min(1)) (poca_trainer.py:706-745,
+    option_critic_trainer.py:515-525); on the GPU one kernel each way (_CategoricalTerms)."""
+    M = logits.shape[0]
+    if (FUSED_LOSSES and logits.is_cuda and logits.dtype == torch.float32 and logits.dim() == 2
+            and 1 <= logits.shape[1] <= 64 and actions.numel() == M and M > 0):
+        m = _loss_mask(mask, M) if mask is None or mask.dtype == torch.bool else None
+        d = _loss_denom(denom, logits.device)
+        if m is not None and d is not False:
+            return _CategoricalTerms.apply(logits, actions.reshape(M).long().contiguous(), m[1], d)
+    dist = torch.distributions.Categorical(validate_args=False, logits=logits)
+    logp = dist.log_prob(actions.reshape(M).long())
+    ent = dist.entropy()
+    if mask is None:
+        return logp, (ent.mean() if denom is None else ent.sum() / denom)
+    return logp, (ent * mask).sum() / (denom if denom is not None else mask.sum().clamp_min(1))
+
+
 def trust_region_value_loss(values, old_values, returns, epsilon: float, mask=None, denom=None):
     """ML-Agents trust_region_value_loss (poca_trainer.py:144-162); on the GPU one kernel each
     way (_ValueLoss)."""

@@ -25,9 +25,9 @@ from __future__ import annotations
 
 import torch
 import torch.optim as optim
-from torch.distributions import Bernoulli, Categorical
+from torch.distributions import Bernoulli
 
-from ._trainer import TrainerBase, trust_region_value_loss
+from ._trainer import TrainerBase, categorical_terms, trust_region_value_loss
 from .config import PAPER_PARITY_VERSION, FixedOptionCriticConfig
 from .option_collector import FixedOptionCollector
 from .option_critic_buffer import FixedOptionRolloutBuffer
@@ -149,19 +149,17 @@ class FixedOptionCriticTrainer(TrainerBase):
             sequence_length=L, passes=("value", "joint", "baseline"))
         option_logits, c_out = self._manager_sequence(batch, c_item)
         new_team_values, new_joint, new_baselines = self.critic.sequence_passes_end(c_out, c_ctx)
-        opt_dist = Categorical(validate_args=False, logits=option_logits.reshape(B * L, O))
-        new_logp = opt_dist.log_prob(options.reshape(-1)).view(B, L)
-        ent = opt_dist.entropy().view(B, L)
         # PPO clip over the switch decisions (option_mask) inside the loss mask (OCT:515-525)
         mask_flat = (batch["option_masks"].reshape(-1) > 0.5) & loss_mask.reshape(-1)
         nonterminal = 1.0 - dones
         term_mask = nonterminal * loss_mask
         d_pol, d_mask, d_term = self._denominators([mask_flat.sum(), loss_mask.sum(), term_mask.sum()])
         n_pol = d_pol if d_pol is not None else mask_flat.sum().clamp_min(1)
-        n_mask = d_mask if d_mask is not None else loss_mask.sum().clamp_min(1)
         n_term = d_term if d_term is not None else term_mask.sum().clamp_min(1)
-
-        option_entropy = (ent * loss_mask).sum() / n_mask
+        # Categorical(option logits).log_prob(options) and the masked mean option entropy
+        new_logp, option_entropy = categorical_terms(option_logits.reshape(B * L, O), options.reshape(-1),
+                                                     loss_mask.reshape(-1), d_mask)
+        new_logp = new_logp.view(B, L)
         adv = batch["advantages"].reshape(-1).detach()
         ratio = (new_logp.reshape(-1) - batch["old_option_log_probs"].reshape(-1)).exp()
         pg = torch.min(ratio * adv, ratio.clamp(1.0 - current_eps, 1.0 + current_eps) * adv)

@@ -29,7 +29,7 @@ import itertools
 import torch
 import torch.optim as optim
 
-from ._trainer import (PolynomialDecay, TrainerBase, masked_mean, stack_obs, trust_region_policy_loss,
+from ._trainer import (PolynomialDecay, TrainerBase, categorical_terms, masked_mean, stack_obs, trust_region_policy_loss,
                        trust_region_value_loss)
 from .checkpoint import load_poca_checkpoint, poca_checkpoint
 from .collector import POCARolloutCollector
@@ -145,7 +145,8 @@ class POCATrainer(TrainerBase):
         """The recurrent actor over the minibatch sequences with the memory of rows whose
         episode ended at t zeroed before step t+1 (the per-step loop of PT:706-723, as one
         masked sequence: one swarm_lstm_seq launch each way on the GPU). `other_item`: an
-        independent LSTM item (the critic's) run in the same launch; its output is returned."""
+        independent LSTM item (the critic's) run in the same launch; its output is returned.
+        Returns (logits (B*L, A), actions (B*L,), the other item's output)."""
         obs, actions = batch["obs"], batch["actions"]
         B, L = obs.shape[:2]
         state = (batch["memory_h"].unsqueeze(0).detach(), batch["memory_c"].unsqueeze(0).detach())
@@ -154,9 +155,7 @@ class POCATrainer(TrainerBase):
             items.append(other_item)
         outs = lstm_sequences(items)
         logits = self.actor.logits_head(outs[0][0])
-        dist = torch.distributions.Categorical(validate_args=False, logits=logits.reshape(B * L, -1))
-        logp = dist.log_prob(actions.reshape(B * L).long()).view(B, L, 1)
-        return logp, dist.entropy().view(B, L), (outs[1][0] if other_item is not None else None)
+        return logits.reshape(B * L, -1), actions.reshape(B * L), (outs[1][0] if other_item is not None else None)
 
     def _compute_recurrent_losses(self, batch: dict, current_eps: float):
         """poca_trainer.py:690-775."""
@@ -176,14 +175,15 @@ class POCATrainer(TrainerBase):
              "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
                           batch["baseline_memory_c"].unsqueeze(0).detach())},
             sequence_length=L, passes=("value", "baseline"))
-        logp_seq, ent_seq, c_out = self._actor_sequence(batch, c_item)
+        logits, act, c_out = self._actor_sequence(batch, c_item)
         new_tv, new_bl = self.critic.sequence_passes_end(c_out, c_ctx)
         (d_mask,) = self._denominators([loss_mask.sum()])
+        # Categorical(logits).log_prob(actions) and the masked mean entropy (PT:724-745)
+        logp, mean_entropy = categorical_terms(logits, act, loss_mask.reshape(-1), d_mask)
         policy_loss = trust_region_policy_loss(batch["advantages"].unsqueeze(-1).reshape(-1, 1),
-                                               logp_seq.reshape(-1, logp_seq.shape[-1]),
+                                               logp.reshape(-1, 1),
                                                batch["old_log_probs"].reshape(-1, batch["old_log_probs"].shape[-1]),
                                                current_eps, loss_mask.reshape(-1), denom=d_mask)
-        mean_entropy = (ent_seq * loss_mask).sum() / (d_mask if d_mask is not None else loss_mask.sum().clamp_min(1))
         flat_mask = loss_mask.reshape(B * L)
         value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
                                              batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)

@@ -110,3 +110,30 @@ def test_loss_kernels_refuse_bad_arguments(gpu_device):
     assert lib.swarm_ppo_value_loss(0, p, p, p, None, None, 0.2, None, p, p, None) != 0
     assert lib.swarm_ppo_value_loss(8, p, p, p, p, m.data_ptr(), 0.2, None, p, p, None) != 0
     assert lib.swarm_ppo_policy_loss(4, 2, 3, p, p, p, None, None, 0.8, 1.2, 0, None, p, p, None) != 0
+
+
+@pytest.mark.parametrize("K,mask_kind,with_denom", [(6, "bool", False), (6, "bool", True), (6, None, False),
+                                                    (18, "bool", False), (1, "bool", False)])
+def test_categorical_terms(K, mask_kind, with_denom, gpu_device):
+    """log_prob and the masked mean entropy of Categorical(logits) (swarm_categorical_terms*) against
+    torch.distributions.Categorical, forward and the logits' gradient (both outputs weighted)."""
+    from SwarmACB_isaac.agents._trainer import categorical_terms
+
+    M = 2048
+    g = torch.Generator(device=gpu_device).manual_seed(K * 3 + int(with_denom))
+    z0 = torch.randn(M, K, device=gpu_device, generator=g) * 2.0
+    z0[:8] = 0.0                                     # uniform rows
+    acts = torch.randint(0, K, (M,), device=gpu_device, generator=g)
+    mask = _mask(mask_kind, M, g, gpu_device)
+    denom = torch.tensor(1500.0, device=gpu_device) if with_denom else None
+    glp = torch.randn(M, device=gpu_device, generator=g)
+    out = []
+    for fused in (True, False):
+        z = z0.clone().requires_grad_(True)
+        lp, ent = _run(categorical_terms, fused, z, acts, mask, denom)
+        (lp * glp).sum().backward(retain_graph=True)
+        (ent * 0.37).backward()
+        out.append((lp.detach(), ent.detach(), z.grad.clone()))
+    _close(out[0][0], out[1][0], 1e-6, "log_prob")
+    _close(out[0][1], out[1][1], 1e-6, "mean entropy")
+    _close(out[0][2], out[1][2], 2e-6, "d logits")
