@@ -149,8 +149,9 @@ FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of
 FUSED_ATTENTION = True   # False: ResidualSelfAttention's core runs torch's bmm / softmax path
 # False (or SWARM_FUSED_NORMS=0): its LayerNorms, residual add and set mean run torch's ops
 FUSED_NORMS = os.environ.get("SWARM_FUSED_NORMS", "1") != "0"
-# False (or SWARM_FUSED_ENTITIES=0): the critic's training-time entity sets are built by its encoder modules
-FUSED_ENTITIES = os.environ.get("SWARM_FUSED_ENTITIES", "1") != "0"
+# True (SWARM_FUSED_ENTITIES=1): the critic's training-time entity sets on swarm_entity_sets_* (off by
+# default until its measured gain holds; the encoder modules build them otherwise)
+FUSED_ENTITIES = os.environ.get("SWARM_FUSED_ENTITIES", "0") == "1"
 
 
 def _plain_lstm(lstm: nn.LSTM) -> bool:
@@ -340,7 +341,7 @@ class _EntitySets(torch.autograd.Function):
     gradients (per-slab partials summed by swarm_splitk_finish). States and actions carry no
     gradient."""
 
-    SLAB = 256
+    SLAB = 128   # set rows per partial-sum slab (8 row lanes x 16 rows at H = 128)
 
     @staticmethod
     def forward(ctx, states, actions, focal, w_s, b_s, w_sa, b_sa, codes, H):

@@ -88,22 +88,25 @@ __global__ __launch_bounds__(kThreads) void entity_fwd_kernel(Geo g, const float
     out[row * g.H + h] = silu(y);
 }
 
-// block = one slab of set rows, thread = output column h (row lanes = kThreads / H); per-thread
-// partials of dW_s[h][:], db_s[h], dW_sa[h][:], db_sa[h], reduced over the row lanes through LDS and
-// written as one slab row of the partial matrix [slab][n_params] (n_params = H(S+1) + H(S+A+1), in
-// the layout dW_s | db_s | dW_sa | db_sa)
-__global__ __launch_bounds__(kThreads) void entity_bwd_kernel(Geo g, int slab, const float* __restrict__ states,
-                                                              const float* __restrict__ actions,
-                                                              const int64_t* __restrict__ focal,
-                                                              const float* __restrict__ ws, const float* __restrict__ bs,
-                                                              const float* __restrict__ wsa,
-                                                              const float* __restrict__ bsa,
-                                                              const float* __restrict__ dout,
-                                                              float* __restrict__ partial) {
-    __shared__ float red[kThreads * (2 * kMaxIn + 2) / 2];   // lanes >= 1 park their partials here
-    const int lanes = kThreads / g.H;
+// block = one slab of set rows; thread = (output column h, row lane) with kBwdThreads / H row lanes,
+// lane l taking rows l, l + lanes, ... of the slab; per-thread partials of dW_s[h][:], db_s[h],
+// dW_sa[h][:], db_sa[h] are reduced over the row lanes through LDS one parameter at a time and written
+// as one slab row of the partial matrix [slab][n_params] (n_params = H(S+1) + H(S+A+1), in the layout
+// dW_s | db_s | dW_sa | db_sa)
+constexpr int kBwdThreads = 1024;
+
+__global__ __launch_bounds__(kBwdThreads) void entity_bwd_kernel(Geo g, int slab, const float* __restrict__ states,
+                                                                 const float* __restrict__ actions,
+                                                                 const int64_t* __restrict__ focal,
+                                                                 const float* __restrict__ ws,
+                                                                 const float* __restrict__ bs,
+                                                                 const float* __restrict__ wsa,
+                                                                 const float* __restrict__ bsa,
+                                                                 const float* __restrict__ dout,
+                                                                 float* __restrict__ partial) {
+    __shared__ float red[kBwdThreads];
+    const int lanes = kBwdThreads / g.H;
     const int h = threadIdx.x % g.H, lane = threadIdx.x / g.H;
-    const int KS = g.S + 1, KSA = g.S + g.A + 1, KT = KS + KSA;
     float accs[kMaxIn + 1], acca[kMaxIn + 1];
 #pragma unroll
     for (int k = 0; k <= kMaxIn; ++k) {
@@ -113,78 +116,62 @@ __global__ __launch_bounds__(kThreads) void entity_bwd_kernel(Geo g, int slab, c
     const int64_t total = (int64_t)g.P * g.B * g.N;
     const int64_t r0 = (int64_t)blockIdx.x * slab;
     const int64_t r1 = min(total, r0 + slab);
-    if (lane < lanes) {
-        for (int64_t row = r0 + lane; row < r1; row += lanes) {
-            const int n = (int)(row % g.N);
-            const int64_t pb = row / g.N;
-            const int p = (int)(pb / g.B);
-            const int64_t b = pb - (int64_t)p * g.B;
-            const int code = g.codes[p];
-            int agent, enc;
-            member_src(g, code, n, code == 2 ? focal[b] : 0, agent, enc);
-            const float* s = states + (b * g.N + agent) * g.S;
-            const float d = dout[row * g.H + h];
-            // inputs of this member as one K-vector (states, then actions for the second encoder);
-            // compile-time indices keep the accumulators in registers
-            float x[kMaxIn];
-            const int K = enc == 0 ? g.S : g.S + g.A;
-            const float* a = enc == 0 ? s : actions + (b * g.N + agent) * g.A;
+    for (int64_t row = r0 + lane; row < r1; row += lanes) {
+        const int n = (int)(row % g.N);
+        const int64_t pb = row / g.N;
+        const int p = (int)(pb / g.B);
+        const int64_t b = pb - (int64_t)p * g.B;
+        const int code = g.codes[p];
+        int agent, enc;
+        member_src(g, code, n, code == 2 ? focal[b] : 0, agent, enc);
+        const float* s = states + (b * g.N + agent) * g.S;
+        const float d = dout[row * g.H + h];
+        // inputs of this member as one K-vector (states, then actions for the second encoder);
+        // compile-time indices keep the accumulators in registers
+        float x[kMaxIn];
+        const int K = enc == 0 ? g.S : g.S + g.A;
+        const float* a = enc == 0 ? s : actions + (b * g.N + agent) * g.A;
 #pragma unroll
-            for (int k = 0; k < kMaxIn; ++k) x[k] = k < g.S ? s[k] : (k < K ? a[k - g.S] : 0.0f);
-            const float* w = enc == 0 ? ws + (int64_t)h * g.S : wsa + (int64_t)h * (g.S + g.A);
-            float acc = 0.0f;
+        for (int k = 0; k < kMaxIn; ++k) x[k] = k < g.S ? s[k] : (k < K ? a[k - g.S] : 0.0f);
+        const float* w = enc == 0 ? ws + (int64_t)h * g.S : wsa + (int64_t)h * (g.S + g.A);
+        float acc = 0.0f;
 #pragma unroll
-            for (int k = 0; k < kMaxIn; ++k)
-                if (k < K) acc += x[k] * w[k];
-            const float y = acc + (enc == 0 ? bs[h] : bsa[h]);
-            const float sg = 1.0f / (1.0f + expf(-y));
-            const float dy = d * (sg * (1.0f + y * (1.0f - sg)));
-            if (enc == 0) {
+        for (int k = 0; k < kMaxIn; ++k)
+            if (k < K) acc += x[k] * w[k];
+        const float y = acc + (enc == 0 ? bs[h] : bsa[h]);
+        const float sg = 1.0f / (1.0f + expf(-y));
+        const float dy = d * (sg * (1.0f + y * (1.0f - sg)));
+        if (enc == 0) {
 #pragma unroll
-                for (int k = 0; k < kMaxIn; ++k) accs[k] += dy * x[k];   // x[k] = 0 beyond S
-                accs[kMaxIn] += dy;
-            } else {
+            for (int k = 0; k < kMaxIn; ++k) accs[k] += dy * x[k];   // x[k] = 0 beyond S
+            accs[kMaxIn] += dy;
+        } else {
 #pragma unroll
-                for (int k = 0; k < kMaxIn; ++k) acca[k] += dy * x[k];
-                acca[kMaxIn] += dy;
-            }
+            for (int k = 0; k < kMaxIn; ++k) acca[k] += dy * x[k];
+            acca[kMaxIn] += dy;
         }
     }
-    // row lanes 1.. park their partials, lane 0 adds them in lane order and writes the slab row
-    float* mine = red + (int64_t)(threadIdx.x - g.H) * KT;
-    if (lane >= 1 && lane < lanes) {
-#pragma unroll
-        for (int k = 0; k < kMaxIn; ++k) {
-            if (k < g.S) mine[k] = accs[k];
-            if (k < g.S + g.A) mine[KS + k] = acca[k];
+    const int64_t n_params = (int64_t)g.H * (g.S + 1) + (int64_t)g.H * (g.S + g.A + 1);
+    float* dst = partial + (int64_t)blockIdx.x * n_params;
+    float* d2 = dst + (int64_t)g.H * (g.S + 1);
+    // one parameter column at a time: every lane parks its partial, lane 0 adds them in lane order
+    auto reduce_out = [&](float v, float* out) {
+        red[threadIdx.x] = v;
+        __syncthreads();
+        if (lane == 0) {
+            float t = red[h];
+            for (int l = 1; l < lanes; ++l) t += red[l * g.H + h];
+            *out = t;
         }
-        mine[g.S] = accs[kMaxIn];
-        mine[KS + g.S + g.A] = acca[kMaxIn];
+        __syncthreads();
+    };
+#pragma unroll
+    for (int k = 0; k < kMaxIn; ++k) {
+        if (k < g.S) reduce_out(accs[k], dst + (int64_t)h * g.S + k);
+        if (k < g.S + g.A) reduce_out(acca[k], d2 + (int64_t)h * (g.S + g.A) + k);
     }
-    __syncthreads();
-    if (lane == 0) {
-        for (int l = 1; l < lanes; ++l) {
-            const float* o = red + (int64_t)(l * g.H + h - g.H) * KT;
-#pragma unroll
-            for (int k = 0; k < kMaxIn; ++k) {
-                if (k < g.S) accs[k] += o[k];
-                if (k < g.S + g.A) acca[k] += o[KS + k];
-            }
-            accs[kMaxIn] += o[g.S];
-            acca[kMaxIn] += o[KS + g.S + g.A];
-        }
-        const int64_t n_params = (int64_t)g.H * KT;
-        float* dst = partial + (int64_t)blockIdx.x * n_params;
-        // dW_s [H][S] | db_s [H] | dW_sa [H][S+A] | db_sa [H]
-        float* d2 = dst + (int64_t)g.H * KS;
-#pragma unroll
-        for (int k = 0; k < kMaxIn; ++k) {
-            if (k < g.S) dst[(int64_t)h * g.S + k] = accs[k];
-            if (k < g.S + g.A) d2[(int64_t)h * (g.S + g.A) + k] = acca[k];
-        }
-        dst[(int64_t)g.H * g.S + h] = accs[kMaxIn];
-        d2[(int64_t)g.H * (g.S + g.A) + h] = acca[kMaxIn];
-    }
+    reduce_out(accs[kMaxIn], dst + (int64_t)g.H * g.S + h);
+    reduce_out(acca[kMaxIn], d2 + (int64_t)g.H * (g.S + g.A) + h);
 }
 
 int32_t check_geo(int64_t B, int32_t N, int32_t S, int32_t A, int32_t H, int32_t P, const int32_t* codes) {
@@ -240,7 +227,7 @@ int32_t swarm_entity_sets_backward(int64_t B, int32_t N, int32_t S, int32_t A, i
     const int64_t rows = (int64_t)P * B * N;
     const int64_t slabs = (rows + slab - 1) / slab;
     if (slabs > 0x7fffffff) return SWARM_ERR_ARG;
-    entity_bwd_kernel<<<(unsigned)slabs, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+    entity_bwd_kernel<<<(unsigned)slabs, kBwdThreads, 0, static_cast<hipStream_t>(stream)>>>(
         g, slab, states, actions, focal, w_s, b_s, w_sa, b_sa, d_out, partials);
     return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP;
 }

@@ -30,6 +30,7 @@ def test_entity_sets_match_module_path(passes, S, A, gpu_device):
     focal = torch.randint(0, N, (B,), device=gpu_device, generator=g)
     d_out = torch.randn(len(passes) * B, N, 128, device=gpu_device, generator=g)
     res = []
+    prev = pn.FUSED_ENTITIES
     for fused in (True, False):
         pn.FUSED_ENTITIES = fused
         try:
@@ -52,7 +53,7 @@ def test_entity_sets_match_module_path(passes, S, A, gpu_device):
                      for p in list(critic.obs_entity_enc.parameters()) + list(critic.obs_act_entity_enc.parameters())]
             res.append((ents.detach(), grads))
         finally:
-            pn.FUSED_ENTITIES = True
+            pn.FUSED_ENTITIES = prev
     _close(res[0][0], res[1][0], 1e-6, "entity sets")
     for k, (a, b) in enumerate(zip(res[0][1], res[1][1])):
         if b is None:
