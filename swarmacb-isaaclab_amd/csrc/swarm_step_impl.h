@@ -1418,7 +1418,7 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<LY>& S, bool with_
 template <int MISSION, int PROFILE, int LY, int C>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
-                                        float& cyw) {
+                                        float& cyw, const uint4* early_rb = nullptr) {
     SWARM_PH_T(wt_t);
     publish<LY>(g, L, S, x, y);
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
@@ -1437,7 +1437,8 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
         obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
-        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+        if (early_rb) rb = *early_rb;   // drawn at the top of the substep (SWARM_OBS_FUSE == 2)
+        else if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
     }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
@@ -1740,6 +1741,11 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         const float* u_obs = rp.rab ? rp.rab + ((size_t)s * L.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
         TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, (size_t)EN, (size_t)q, tick};
 
+        // SWARM_OBS_FUSE == 2: this substep's packet-loss block drawn before the physics, so its
+        // multiply chain overlaps the drive and the contact solver (same counter, same draws)
+        constexpr bool EARLY_RB = SWARM_OBS_FUSE == 2 && !REPLAY && C > 0 && ChunkRng<C>::K18;
+        uint4 rb_obs = make_uint4(0, 0, 0, 0);
+        if constexpr (EARLY_RB) rb_obs = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
         // ------------------------------ actions ------------------------------
         SWARM_PH_T(wt_t);
         float lw, rw;
@@ -1834,7 +1840,8 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw);
+        observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw,
+                                         EARLY_RB ? &rb_obs : nullptr);
     }
 
     // ---- store state and per-call outputs (wave 0; all waves hold the same values) ----
