@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--prewarm", type=float, default=1.0,
                     help="seconds of untimed step launches on the timed engine before the warm-up "
                          "(steady clocks, arenas past the post-spawn contact burst; steps/warmup unchanged)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: the timed decisions are captured once as a HIP graph (with timing events as graph "
+                         "nodes at both ends) and replayed inside the timed region; 0: eager launches")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
@@ -249,20 +252,41 @@ def main():
         eng.step(acts[d], dp, out=out)
     torch.cuda.synchronize(dev)
 
-    # HIP events on the launch stream bracket the whole timed region (not every launch:
-    # each event is a packet of its own in the stream, and a pair per decision added
-    # ~5 us of GPU-side gap per launch); the per-launch average includes the gaps between
-    # back-to-back launches, so it is an upper bound on the kernel's own duration.
+    # HIP events bracket the whole timed region (not every launch: each event is a packet of
+    # its own in the stream, and a pair per decision added ~5 us of GPU-side gap per launch);
+    # the per-launch average includes the gaps between back-to-back launches, so it is an
+    # upper bound on the kernel's own duration.
+    # --graph 1 (default): the n_dec timed launches are captured ONCE (nothing executes during
+    # capture; the engine's host state - Philox tick, episode-length mirror - advances exactly as
+    # the eager loop would) as one HIP graph whose first and last nodes are the two timing
+    # events, and the graph is replayed once inside the timed region. The events then see only
+    # the GPU's own work: with few timed launches (the driver's 4) eager events also counted
+    # the host's launch latency after the first event (BENCH_r03: 68.3 vs 59.5 us rocprofv3).
+    # The value stays wall-clock around the replay.
     stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    graph = None
+    if args.graph:
+        ev0 = torch.cuda.Event(enable_timing=True, external=True)
+        ev1 = torch.cuda.Event(enable_timing=True, external=True)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            ev0.record()
+            for d in range(n_dec):
+                eng.step(acts[n_warm + d], dp, out=out)
+            ev1.record()
+    else:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for d in range(n_dec):
-        eng.step(acts[n_warm + d], dp, out=out)
-    ev1.record(stream)
+    if graph is not None:
+        graph.replay()
+    else:
+        ev0.record(stream)
+        for d in range(n_dec):
+            eng.step(acts[n_warm + d], dp, out=out)
+        ev1.record(stream)
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -308,6 +332,8 @@ def main():
                 "global_envs": world * E,
                 "decision_period": dp,
                 "layout": args.layout or "default",
+                "timed_launches": "one HIP graph of the timed decisions, replayed once" if graph is not None
+                                  else "eager launches",
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,
             },

@@ -167,35 +167,16 @@ int32_t swarm_ppo_policy_loss_backward(int64_t M, int32_t A, int32_t adv_cols, c
  * logits (K <= 64) and the taken actions (int64), log_probs[m] = z[m][a_m] - logsumexp(z[m]) and
  * *mean_entropy = sum_m H_m active_m / (*denom if denom else max(sum active, 1)), H = -sum_k p_k log p_k,
  * active = mask_u8 (NULL: all rows, denominator M). *used_denom is the denominator used (for the backward).
+ * An action outside [0, K) on ANY row (masked or not: torch's gather refuses it too) gets log_probs NaN and
+ * sets *bad_actions (a device int32 the caller zeroes and reads, or NULL) to 1.
  * The backward writes d_logits = g_log_probs[m] (onehot(a_m) - p) + *g_mean_entropy active_m / denom
  * (-p (log p + H)); either gradient pointer may be NULL (= 0). */
 int32_t swarm_categorical_terms(int64_t M, int32_t K, const float* logits, const int64_t* actions,
                                 const uint8_t* mask_u8, const float* denom, float* log_probs, float* mean_entropy,
-                                float* used_denom, void* stream);
+                                float* used_denom, int32_t* bad_actions, void* stream);
 int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logits, const int64_t* actions,
                                          const uint8_t* mask_u8, const float* used_denom, const float* g_log_probs,
                                          const float* g_mean_entropy, float* d_logits, void* stream);
-
-/* The critic's entity sets of a minibatch's training passes (POCACritic, reference
- * agents/poca_networks.py:597-820): for P passes (pass_codes[p]: 0 = critic_pass sets, member n ->
- * enc_s(s_n); 1 = joint_action_pass sets, member n -> enc_sa([s_n, a_n]); 2 = focal baseline sets, member
- * 0 -> enc_s(s_f), member k >= 1 -> enc_sa([s_o, a_o]) with o = (k-1) + (k-1 >= f), f = focal[b]) over B
- * rows of N agents, out[(p*B + b)*N + n][:] = SiLU(W x + bias) with enc_s = (w_s [H][S], b_s), enc_sa =
- * (w_sa [H][S+A], b_sa); states [B][N][S], actions [B][N][A], focal [B] int64. S + A <= 32, H in {128, 256},
- * P <= SWARM_ENTITY_MAX_PASSES (pass_codes is a HOST array).
- * The backward writes, per slab of `slab` set rows, the partial sums of the encoders' parameter gradients
- * from d_out into partials [slabs][H(S+1) + H(S+A+1)] (layout dW_s | db_s | dW_sa | db_sa); the caller
- * sums them over the slabs with swarm_splitk_finish. */
-#define SWARM_ENTITY_MAX_PASSES 4
-int32_t swarm_entity_sets_forward(int64_t B, int32_t N, int32_t S, int32_t A, int32_t H, int32_t P,
-                                  const int32_t* pass_codes, const float* states, const float* actions,
-                                  const int64_t* focal, const float* w_s, const float* b_s, const float* w_sa,
-                                  const float* b_sa, float* out, void* stream);
-int32_t swarm_entity_sets_backward(int64_t B, int32_t N, int32_t S, int32_t A, int32_t H, int32_t P,
-                                   const int32_t* pass_codes, const float* states, const float* actions,
-                                   const int64_t* focal, const float* w_s, const float* b_s, const float* w_sa,
-                                   const float* b_sa, const float* d_out, int32_t slab, float* partials,
-                                   void* stream);
 
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]

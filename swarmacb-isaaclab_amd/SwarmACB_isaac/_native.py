@@ -75,9 +75,7 @@ TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa
                  "swarm_set_pool_forward", "swarm_set_pool_backward", "swarm_splitk_colsum",
                  "swarm_splitk_finish", "swarm_ppo_value_loss", "swarm_ppo_value_loss_backward",
                  "swarm_ppo_policy_loss", "swarm_ppo_policy_loss_backward", "swarm_categorical_terms",
-                 "swarm_categorical_terms_backward", "swarm_entity_sets_forward", "swarm_entity_sets_backward"]
-ENTITY_MAX_PASSES = 4      # SWARM_ENTITY_MAX_PASSES (include/swarmtrain.h)
-ENTITY_MAX_INPUTS = 32     # state + action features of swarm_entity_sets_*
+                 "swarm_categorical_terms_backward"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 
@@ -203,13 +201,9 @@ def load() -> C.CDLL:
     lib.swarm_ppo_policy_loss_backward.restype = i32
     lib.swarm_ppo_policy_loss_backward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp]
     lib.swarm_categorical_terms.restype = i32
-    lib.swarm_categorical_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.swarm_categorical_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_categorical_terms_backward.restype = i32
     lib.swarm_categorical_terms_backward.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
-    lib.swarm_entity_sets_forward.restype = i32
-    lib.swarm_entity_sets_forward.argtypes = [i64, i32, i32, i32, i32, i32, vp] + [vp] * 9
-    lib.swarm_entity_sets_backward.restype = i32
-    lib.swarm_entity_sets_backward.argtypes = [i64, i32, i32, i32, i32, i32, vp] + [vp] * 8 + [i32, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:
         raise RuntimeError(f"libswarmstep ABI {lib.swarm_abi_version()} != expected {ABI_VERSION}")
     _lib = lib

@@ -188,7 +188,8 @@ class _CategoricalTerms(torch.autograd.Function):
         used = torch.empty((), dtype=z.dtype, device=z.device)
         stream = C.c_void_p(torch.cuda.current_stream(z.device).cuda_stream)
         _native.check(_native.load().swarm_categorical_terms(M, K, _vp(z), _vp(actions), _vp(mask_u), _vp(denom),
-                                                             _vp(lp), _vp(ent), _vp(used), stream),
+                                                             _vp(lp), _vp(ent), _vp(used),
+                                                             _vp(_bad_action_flag(z.device)), stream),
                       "swarm_categorical_terms")
         ctx.save_for_backward(z, actions, mask_u, used)
         return lp, ent
@@ -205,6 +206,30 @@ class _CategoricalTerms(torch.autograd.Function):
             _vp(g_ent.reshape(()).contiguous()) if g_ent is not None else None, _vp(dz), stream),
             "swarm_categorical_terms_backward")
         return dz, None, None, None
+
+
+_BAD_ACTIONS: dict = {}
+
+
+def _bad_action_flag(device) -> torch.Tensor:
+    """The device int32 swarm_categorical_terms sets when an action is outside [0, K) (one per
+    device, allocated before any graph capture by the first eager step)."""
+    key = str(device)
+    if key not in _BAD_ACTIONS:
+        _BAD_ACTIONS[key] = torch.zeros(1, dtype=torch.int32, device=device)
+    return _BAD_ACTIONS[key]
+
+
+def check_categorical_actions(device) -> None:
+    """Raise if a categorical term of this device saw an action outside [0, K) since the last
+    check (torch's Categorical.log_prob / gather raises on such an index; the fused kernel flags
+    it instead of returning a silent NaN). One host read, called once per update."""
+    flag = _BAD_ACTIONS.get(str(device))
+    if flag is not None and int(flag.item()):
+        flag.zero_()
+        raise IndexError("categorical policy terms: an action / option index outside [0, K) reached the "
+                         "update (e.g. the -1 'fresh option' sentinel); torch.distributions.Categorical "
+                         "would raise on it too")
 
 
 def categorical_terms(logits, actions, mask=None, denom=None):

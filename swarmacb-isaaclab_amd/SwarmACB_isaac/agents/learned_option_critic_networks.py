@@ -46,7 +46,7 @@ class SquashedNormal:
 
     _EPS = 1e-6
 
-    def __init__(self, loc: torch.Tensor, scale: torch.Tensor, validate_args: bool | None = None):
+    def __init__(self, loc: torch.Tensor, scale: torch.Tensor, validate_args: bool = False):
         self.loc, self.scale = loc, scale
         self.base_dist = Normal(loc, scale, validate_args=validate_args)
 

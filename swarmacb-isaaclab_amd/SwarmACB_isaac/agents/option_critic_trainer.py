@@ -27,7 +27,7 @@ import torch
 import torch.optim as optim
 from torch.distributions import Bernoulli
 
-from ._trainer import TrainerBase, categorical_terms, trust_region_value_loss
+from ._trainer import TrainerBase, categorical_terms, check_categorical_actions, trust_region_value_loss
 from .config import PAPER_PARITY_VERSION, FixedOptionCriticConfig
 from .option_collector import FixedOptionCollector
 from .option_critic_buffer import FixedOptionRolloutBuffer
@@ -248,6 +248,7 @@ class FixedOptionCriticTrainer(TrainerBase):
             switch = self.comm.sum_tensor(switch)
         n = max(n_updates, 1)
         out = {k: v / n for k, v in zip(LOSS_KEYS, totals.tolist())}
+        check_categorical_actions(self.device)
         out.update(lr=self.current_lr, eps=self.current_eps, beta=self.current_beta,
                    switch_rate=float(switch[0] / switch[1].clamp_min(1)),
                    option_usage=(counts / counts.sum().clamp(min=1.0)).tolist())

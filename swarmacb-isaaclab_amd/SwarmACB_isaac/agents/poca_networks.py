@@ -149,9 +149,6 @@ FUSED_LSTM = True   # False: every LSTM call runs torch's nn.LSTM (benchmarks of
 FUSED_ATTENTION = True   # False: ResidualSelfAttention's core runs torch's bmm / softmax path
 # False (or SWARM_FUSED_NORMS=0): its LayerNorms, residual add and set mean run torch's ops
 FUSED_NORMS = os.environ.get("SWARM_FUSED_NORMS", "1") != "0"
-# True (SWARM_FUSED_ENTITIES=1): the critic's training-time entity sets on swarm_entity_sets_* (off by
-# default until its measured gain holds; the encoder modules build them otherwise)
-FUSED_ENTITIES = os.environ.get("SWARM_FUSED_ENTITIES", "0") == "1"
 
 
 def _plain_lstm(lstm: nn.LSTM) -> bool:
@@ -332,57 +329,6 @@ class _SetPool(torch.autograd.Function):
         _native.check(lib.swarm_set_pool_backward(S, n, xhat.shape[1], _ptr(dpooled.contiguous()), _ptr(xhat),
                                                   _ptr(rstd), _ptr(dz), stream), "swarm_set_pool_backward")
         return dz, dz, None, None
-
-
-class _EntitySets(torch.autograd.Function):
-    """The entity sets of a minibatch's critic passes on swarm_entity_sets_forward / _backward
-    (include/swarmtrain.h): SiLU(W x + b) of the state-only and the state + action encoders written
-    straight into the stacked (P*B, N, H) sets; the backward returns the encoders' parameter
-    gradients (per-slab partials summed by swarm_splitk_finish). States and actions carry no
-    gradient."""
-
-    SLAB = 128   # set rows per partial-sum slab (8 row lanes x 16 rows at H = 128)
-
-    @staticmethod
-    def forward(ctx, states, actions, focal, w_s, b_s, w_sa, b_sa, codes, H):
-        B, N, S = states.shape
-        A = actions.shape[-1] if actions is not None else 0
-        P = len(codes)
-        out = torch.empty(P * B, N, H, dtype=states.dtype, device=states.device)
-        arr = (C.c_int32 * P)(*codes)
-        stream = C.c_void_p(torch.cuda.current_stream(states.device).cuda_stream)
-        _native.check(_native.load().swarm_entity_sets_forward(
-            B, N, S, A, H, P, arr, _ptr(states), _ptr(actions), _ptr(focal), _ptr(w_s), _ptr(b_s), _ptr(w_sa),
-            _ptr(b_sa), _ptr(out), stream), "swarm_entity_sets_forward")
-        ctx.save_for_backward(states, actions, focal, w_s, b_s, w_sa, b_sa)
-        ctx.dims = (B, N, S, A, H, tuple(codes))
-        return out
-
-    @staticmethod
-    def backward(ctx, d_out):
-        states, actions, focal, w_s, b_s, w_sa, b_sa = ctx.saved_tensors
-        B, N, S, A, H, codes = ctx.dims
-        P = len(codes)
-        rows = P * B * N
-        slabs = (rows + _EntitySets.SLAB - 1) // _EntitySets.SLAB
-        n_s, n_sa = H * (S + 1), H * (S + A + 1)
-        parts = torch.empty(slabs, n_s + n_sa, dtype=states.dtype, device=states.device)
-        flat = torch.empty(n_s + n_sa, dtype=states.dtype, device=states.device)
-        arr = (C.c_int32 * P)(*codes)
-        lib = _native.load()
-        stream = C.c_void_p(torch.cuda.current_stream(states.device).cuda_stream)
-        _native.check(lib.swarm_entity_sets_backward(
-            B, N, S, A, H, P, arr, _ptr(states), _ptr(actions), _ptr(focal), _ptr(w_s), _ptr(b_s), _ptr(w_sa),
-            _ptr(b_sa), _ptr(d_out.contiguous()), _EntitySets.SLAB, _ptr(parts), stream),
-            "swarm_entity_sets_backward")
-        _native.check(lib.swarm_splitk_finish(slabs, n_s + n_sa, _ptr(parts), _ptr(flat), 0, 0, None, None, stream),
-                      "swarm_splitk_finish")
-        d_ws, d_bs = flat[:H * S].view(H, S), flat[H * S:n_s]
-        uses_sa = any(c != 0 for c in codes)
-        d_wsa = flat[n_s:n_s + H * (S + A)].view(H, S + A) if uses_sa else None
-        d_bsa = flat[n_s + H * (S + A):] if uses_sa else None
-        uses_s = any(c != 1 for c in codes)
-        return (None, None, None, d_ws if uses_s else None, d_bs if uses_s else None, d_wsa, d_bsa, None, None)
 
 
 def lstm_sequence(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):
@@ -930,48 +876,21 @@ class POCACritic(nn.Module):
         for name in passes:
             if name not in ("value", "joint", "baseline"):
                 raise ValueError(f"unknown critic pass {name!r}")
-        ents = self._fused_entity_sets(all_states, all_actions, focal_agent_ids, passes)
-        if ents is None:
-            sets = []
-            for name in passes:
-                if name == "value":
-                    sets.append(self.obs_entity_enc(all_states))
-                elif name == "joint":
-                    sets.append(self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1)))
-                else:
-                    sets.append(self._focal_entities(all_states, all_actions, focal_agent_ids))
-            ents = torch.cat(sets, dim=0)
+        sets = []
+        for name in passes:
+            if name == "value":
+                sets.append(self.obs_entity_enc(all_states))
+            elif name == "joint":
+                sets.append(self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1)))
+            else:
+                sets.append(self._focal_entities(all_states, all_actions, focal_agent_ids))
+        ents = torch.cat(sets, dim=0)
         memory = None
         if self.lstm is not None:
             memory = tuple(torch.cat([memories[name][i] for name in passes], dim=1) for i in (0, 1))
         pooled = self.self_attn(ents)
         encoding, item = self._tail_begin(pooled, memory, sequence_length)
         return item, (encoding, N, B)
-
-    _PASS_CODES = {"value": 0, "joint": 1, "baseline": 2}
-
-    def _fused_entity_sets(self, all_states, all_actions, focal_ids, passes):
-        """The stacked entity sets of `passes` in one swarm_entity_sets_forward launch (_EntitySets),
-        or None when the shapes do not fit it (then the module path builds them)."""
-        enc_s, enc_sa = self.obs_entity_enc.encoder.net, self.obs_act_entity_enc.encoder.net
-        needs_a = any(p != "value" for p in passes)
-        if not (FUSED_ENTITIES and all_states.is_cuda and all_states.dtype == torch.float32
-                and len(passes) <= _native.ENTITY_MAX_PASSES and self.h_size in _native.NORM_WIDTHS
-                and len(enc_s) == 2 and len(enc_sa) == 2 and isinstance(enc_s[1], nn.SiLU)
-                and isinstance(enc_sa[1], nn.SiLU)
-                and all_states.shape[-1] + self.act_dim <= _native.ENTITY_MAX_INPUTS
-                and not all_states.requires_grad
-                and (not needs_a or (all_actions is not None and all_actions.dtype == torch.float32
-                                     and not all_actions.requires_grad
-                                     and all_actions.shape[:2] == all_states.shape[:2]
-                                     and all_actions.shape[-1] == self.act_dim))):
-            return None
-        states = all_states.contiguous()
-        actions = all_actions.contiguous() if needs_a else None
-        focal = focal_ids.long().contiguous() if "baseline" in passes else None
-        lin_s, lin_sa = enc_s[0], enc_sa[0]
-        return _EntitySets.apply(states, actions, focal, lin_s.weight, lin_s.bias, lin_sa.weight, lin_sa.bias,
-                                 [self._PASS_CODES[p] for p in passes], self.h_size)
 
     def sequence_passes_end(self, lstm_out, ctx):
         """The values of sequence_passes from the LSTM output of its item (None without memory)."""

@@ -29,8 +29,8 @@ import itertools
 import torch
 import torch.optim as optim
 
-from ._trainer import (PolynomialDecay, TrainerBase, categorical_terms, masked_mean, stack_obs, trust_region_policy_loss,
-                       trust_region_value_loss)
+from ._trainer import (PolynomialDecay, TrainerBase, categorical_terms, check_categorical_actions, masked_mean,
+                       stack_obs, trust_region_policy_loss, trust_region_value_loss)
 from .checkpoint import load_poca_checkpoint, poca_checkpoint
 from .collector import POCARolloutCollector
 from .config import POCAConfig
@@ -236,6 +236,7 @@ class POCATrainer(TrainerBase):
         if self.comm.active:
             totals = self.comm.sum_tensor(totals) / self.comm.world
         tot = totals.tolist()
+        check_categorical_actions(self.device)
         n = max(n_updates, 1)
         return {"policy_loss": tot[0] / n, "value_loss": tot[1] / n, "baseline_loss": tot[2] / n,
                 "entropy": tot[3] / n, "lr": self.current_lr, "eps": self.current_eps, "beta": self.current_beta}

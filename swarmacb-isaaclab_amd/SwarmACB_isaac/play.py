@@ -46,6 +46,17 @@ def parse(argv=None):
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", type=str, default="cuda:0")
+    # viewer / HUD / Kit options of the reference (play.py:55-83): accepted for command-line
+    # compatibility and ignored (Isaac Sim visuals are out of scope, the run is headless)
+    for flag in ("--fast-viewer", "--exact-env", "--no-editor-hud", "--show-sensors", "--headless",
+                 "--enable_cameras"):
+        ap.add_argument(flag, action="store_true", help=argparse.SUPPRESS)
+    for flag, typ in (("--sim-hz", float), ("--control-hz", float), ("--playback-speed", float),
+                      ("--visual-hz", float), ("--status-interval", float), ("--sensor-robot", int),
+                      ("--sensor-ring-segments", int), ("--sensor-visual-hz", float),
+                      ("--viewer-torch-threads", int), ("--livestream", int), ("--experience", str),
+                      ("--kit_args", str)):
+        ap.add_argument(flag, type=typ, default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 

@@ -359,7 +359,9 @@ __global__ void __launch_bounds__(64 * WAVES) attn_bwd_kernel(int S, int N, int 
 }
 
 bool attn_args_ok(int64_t S, int32_t N, int32_t H, int32_t D) {
-    return S >= 0 && N >= 1 && N <= 32 && H >= 1 && D >= 1 && D % H == 0 && S * H <= 0x7fffffffLL * WAVES &&
+    // S is passed to the kernels as int and every qkv element index ((s N + n) 3D + c) must fit int32
+    return S >= 0 && S <= 0x7fffffffLL && N >= 1 && N <= 32 && H >= 1 && D >= 1 && D % H == 0 &&
+           S * H <= 0x7fffffffLL * WAVES && S * N * 3 * (int64_t)D <= 0x7fffffffLL &&
            (D / H == 32 || D / H == 64 || D / H == 128);
 }
 

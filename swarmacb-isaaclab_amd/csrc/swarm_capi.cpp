@@ -69,7 +69,6 @@ struct swarm_handle {
     std::vector<int32_t> lens;  // per-env host copy, refreshed lazily
     bool lens_exact = true;     // lens[] matches the mirror
     uint8_t* d_mask = nullptr;  // E-byte device scratch for reset masks
-    uint8_t* d_cost = nullptr;  // E-byte per-arena solver work of the last step launch (scheduling hint)
     bool was_reset = false;
     uint64_t last_timeouts = 0;  // substeps of the last swarm_step in which some env timed out
     // env groups of swarm_set_step_groups: one owned stream + join event per group
@@ -83,7 +82,7 @@ namespace {
 
 DevState dev_state(const swarm_state_t* s) {
     return DevState{s->pos_x, s->pos_y, s->yaw, s->fsm, s->wheel_l, s->wheel_r, s->sensor_cache, s->ground_prev,
-                    s->flags, s->episode_length, s->episode_reward, s->completed_reward, s->terminal_critic, nullptr};
+                    s->flags, s->episode_length, s->episode_reward, s->completed_reward, s->terminal_critic};
 }
 
 bool state_ok(const swarm_state_t* s) {
@@ -196,7 +195,6 @@ int32_t swarm_destroy(swarm_handle_t* h) {
     if (!h) return SWARM_ERR_ARG;
     free_groups(h);
     if (h->d_mask) (void)hipFree(h->d_mask);
-    if (h->d_cost) (void)hipFree(h->d_cost);
     delete h;
     return SWARM_OK;
 }
@@ -273,13 +271,7 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     if (h->lens_exact && !h->mirror.buckets.empty())
         h->lens.assign(h->p.num_envs, (int32_t)(h->mirror.buckets.begin()->first + h->mirror.offset));
     const hipStream_t cs = (hipStream_t)stream;
-    if (!h->d_cost) {   // allocated once; written by kernels built with SWARM_PRED_PRIO
-        if (hipMalloc(&h->d_cost, (size_t)h->p.num_envs) != hipSuccess ||
-            hipMemsetAsync(h->d_cost, 0, (size_t)h->p.num_envs, cs) != hipSuccess)
-            return hip_status();
-    }
-    DevState st = dev_state(state);
-    st.cost = h->d_cost;
+    const DevState st = dev_state(state);
     const DevOut o{out->obs, out->reward, out->truncated};
     if (h->groups > 1 && h->g.layout == 103) {
         // fork: every group stream waits for the caller's stream; join: the caller's

@@ -46,14 +46,18 @@ __global__ __launch_bounds__(kThreads) void cat_fwd_kernel(int64_t M, int K, con
                                                            const uint8_t* __restrict__ mask,
                                                            const float* __restrict__ denom,
                                                            float* __restrict__ logp, float* __restrict__ ent,
-                                                           float* __restrict__ used_denom) {
+                                                           float* __restrict__ used_denom,
+                                                           int32_t* __restrict__ bad_actions) {
     __shared__ float rs[kThreads / 64], rn[kThreads / 64];
     float s = 0.0f, n = 0.0f;
     for (int64_t m = threadIdx.x; m < M; m += kThreads) {
         const float* z = logits + m * K;
         const RowStats st = row_stats(z, K);
         const int64_t a = actions[m];
-        logp[m] = (a >= 0 && a < K) ? z[a] - st.lse : NAN;
+        const bool in_range = a >= 0 && a < K;
+        logp[m] = in_range ? z[a] - st.lse : NAN;
+        // torch's gather refuses such an index whatever the mask says: flag it for the caller
+        if (!in_range && bad_actions) atomicOr(bad_actions, 1);
         const float act = mask ? (mask[m] ? 1.0f : 0.0f) : 1.0f;
         s += st.H * act;
         n += act;
@@ -110,11 +114,12 @@ extern "C" {
 
 int32_t swarm_categorical_terms(int64_t M, int32_t K, const float* logits, const int64_t* actions,
                                 const uint8_t* mask_u8, const float* denom, float* log_probs, float* mean_entropy,
-                                float* used_denom, void* stream) {
+                                float* used_denom, int32_t* bad_actions, void* stream) {
     if (M < 1 || K < 1 || K > kMaxK || !logits || !actions || !log_probs || !mean_entropy || !used_denom)
         return SWARM_ERR_ARG;
     cat_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(M, K, logits, actions, mask_u8, denom,
-                                                                        log_probs, mean_entropy, used_denom);
+                                                                        log_probs, mean_entropy, used_denom,
+                                                                        bad_actions);
     return status();
 }
 

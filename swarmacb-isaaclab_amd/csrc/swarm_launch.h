@@ -22,7 +22,6 @@ struct DevState {
     float* ep_rew;
     float* comp_rew;
     float* tcrit;     // [E*N*5]
-    uint8_t* cost;    // [E] library-owned scheduling hint (SWARM_PRED_PRIO) or nullptr
 };
 
 struct DevOut {

@@ -34,14 +34,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "swarm_diag.h"
 #include "swarm_geom.h"
 #include "swarm_launch.h"
-
-// 1: compile-time neighbour chunks are held in registers and processed
-// predicated (fully unrolled); 0: candidate bitmask + ctz loop (smaller code).
-#ifndef SWARM_UNROLLED_CHUNKS
-#define SWARM_UNROLLED_CHUNKS 0
-#endif
 
 // 1: wave-uniform pre-filters skip wall faces / inside tests no lane can need
 // (results unchanged); 0: every face evaluated (reference loop shape).
@@ -72,12 +67,6 @@
 #define SWARM_MIN_WAVES_PER_SIMD 4
 #endif
 
-// Timing-only ablation switches (tools/ablate.sh builds variants with
-// -DSWARM_ABLATE=mask; results are then WRONG by design). 0 in every product build.
-#ifndef SWARM_ABLATE
-#define SWARM_ABLATE 0
-#endif
-
 // Wave priority for arenas with live contacts. A launch lasts as long as its
 // slowest wave, and the slowest waves are the arenas whose contact solver keeps
 // moving robots (up to 25 push iterations per launch against 9 on average,
@@ -91,65 +80,43 @@
 #ifndef SWARM_PRIO_T
 #define SWARM_PRIO_T 2
 #endif
-// Predicted priority (layout 103): each launch stores its arena's count of moving
-// solver iterations (DevState::cost, a library-owned byte per env); the next launch
-// starts at s_setprio 1 / 2 / 3 if that count reached P1 / P2 / P3 (contact
-// clusters persist across decisions), instead of waiting for the graded bumps.
-// The bumps still raise it, never lower it. 0: off. Scheduling only.
-#ifndef SWARM_PRED_PRIO
-#define SWARM_PRED_PRIO 0
-#endif
-#ifndef SWARM_PRED_P1
-#define SWARM_PRED_P1 6
-#endif
-#ifndef SWARM_PRED_P2
-#define SWARM_PRED_P2 10
-#endif
-#ifndef SWARM_PRED_P3
-#define SWARM_PRED_P3 14
-#endif
-
 // 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
 // correction (bitwise = sqrtf); 0: the library's sqrtf.
 #ifndef SWARM_CR_SQRT
 #define SWARM_CR_SQRT 1
 #endif
 
-// 1: the per-lane candidate loops (contact pairs, proximity discs, range-and-bearing
-// terms) are software-pipelined: the LDS read of the next candidate's position is
-// issued before the current candidate's arithmetic, so its latency overlaps the
-// sqrt / rcp chain instead of starting every trip. Same terms in the same order.
-#ifndef SWARM_PIPE_LOOPS
-#define SWARM_PIPE_LOOPS 0
+// 1: the raycast segment table (anchor, direction) is staged once per workgroup in
+// LDS; the proximity rays and the line-of-sight test read a segment with one
+// ds_read_b128 instead of four global loads of the constant table (a per-lane
+// segment index cannot use scalar loads). Same values: bitwise-neutral.
+#ifndef SWARM_SEG_LDS
+#define SWARM_SEG_LDS 0
 #endif
 
-// Verlet-style reuse of the contact candidates across the push iterations of one
-// solver call: the pairs closer than min_dist + margin are listed once and kept
-// until some robot of the arena has moved more than margin / 2 since (a pair's
-// distance then changed by less than the margin, so no contact is missed). The
-// exact sqrt test of every listed pair stays, so results are unchanged.
-// 0: candidates rebuilt every iteration.
-#ifndef SWARM_VERLET
-#define SWARM_VERLET 0
-#endif
-#ifndef SWARM_VERLET_MARGIN
-#define SWARM_VERLET_MARGIN 0.004f
+// 1: ztilde = 1 - 2 / (1 + exp(n)) of the range-and-bearing count n (an integer,
+// ES:452) from a per-workgroup LDS table filled once per launch with the same
+// expression: one ds_read per substep instead of expf + an IEEE division. Bitwise-neutral.
+#ifndef SWARM_ZT_TABLE
+#define SWARM_ZT_TABLE 0
 #endif
 
-// Diagnostic build only (tools/wave_timing.py): each wave of the production step
-// kernel records its start / end shader clock, hardware slot and work counters.
-#ifndef SWARM_WAVE_TIMING
-#define SWARM_WAVE_TIMING 0
+// 1: in the continuous-action Isaac profile the sensor-cache aggregates (the proximity
+// and light vector sums' magnitude / angle: sqrt + atan2) are evaluated only in the
+// last substep of a launch: nothing reads them in between (the behaviour modules are
+// discrete-only) and the cache is stored once per launch. Bitwise-neutral.
+#ifndef SWARM_LAST_CACHE
+#define SWARM_LAST_CACHE 0
 #endif
-// Observation pass of the production kernel (no replay, 6-7-neighbour chunks):
-// the proximity and range-and-bearing candidate masks from ONE read of the
-// part's tile entries, the packet-loss Philox block drawn before the proximity
-// loops (its multiply chain overlaps them), and the line-of-sight direction
-// divided out only when some segment is tested. Same draws, same terms, same
-// order: bitwise-neutral.
-#ifndef SWARM_OBS_FUSE
-#define SWARM_OBS_FUSE 1
+
+// 1: the contact solver's pair term from one hardware reciprocal square root
+// (dist = s * rsq(s), the normal d * rsq(s)) instead of a correctly rounded sqrt
+// and a reciprocal of dist + 1e-8: the same formula within ~2 ulp of dist, i.e.
+// ~1e-8 m per pair push, far inside the 1e-5 teacher-forced contract (NOT bitwise).
+#ifndef SWARM_PAIR_RSQ
+#define SWARM_PAIR_RSQ 0
 #endif
+
 
 namespace swarm {
 
@@ -355,7 +322,36 @@ struct Shared {
     float2 xy[64];
     int ins[64];
     float4 red[4][64 * ly_waves(LY)];
+#if SWARM_SEG_LDS
+    float4 seg[16];     // raycast segments: anchor (x, y), direction (x, y)
+#endif
+#if SWARM_ZT_TABLE
+    float zt[64];       // ztilde of a range-and-bearing count
+#endif
 };
+
+#if SWARM_SEG_LDS
+#define SEG_LDS_PTR(S) ((const float4*)(S).seg)
+#else
+#define SEG_LDS_PTR(S) ((const float4*)nullptr)
+#endif
+
+// Per-workgroup tables staged once per launch (SWARM_SEG_LDS, SWARM_ZT_TABLE). The first
+// read follows publish()'s exchange point, which orders it after these writes.
+template <int LY>
+__device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
+    const int t = threadIdx.x;
+#if SWARM_SEG_LDS
+    if (t < 16) S.seg[t] = t < g.nseg ? make_float4(g.seg_ax[t], g.seg_ay[t], g.seg_sx[t], g.seg_sy[t])
+                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#endif
+#if SWARM_ZT_TABLE
+    if (t < 64) S.zt[t] = 1.0f - 2.0f / (1.0f + expf((float)t));   // rab_finish's expression
+#endif
+    (void)g;
+    (void)S;
+    (void)t;
+}
 
 // Workgroup-wide exchange point of the LDS tile / partial slots. With one wave
 // per workgroup (layouts 1 and 103) the wave's LDS instructions execute in
@@ -429,40 +425,15 @@ __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const fl
     mrab = b;
 }
 
-// f(j, p_j) for every candidate j of this part's chunk (bits of `cand`), in
-// increasing j. SWARM_PIPE_LOOPS: the next candidate's tile entry is read before
-// f runs on the current one.
+// f(j, p_j) for every candidate j of this part's chunk (bits of `cand`), in increasing j.
 template <class F>
 __device__ __forceinline__ void for_each_cand(const Lane& L, const float2* xy, uint32_t cand, F f) {
-#if SWARM_PIPE_LOOPS
-    if (!cand) return;
-    int j = L.j0 + __builtin_ctz(cand);
-    cand &= cand - 1u;
-    float2 p = xy[L.ab + j];
-    for (;;) {
-        const int jn = cand ? L.j0 + __builtin_ctz(cand) : j;
-        const float2 pn = xy[L.ab + jn];
-        f(j, p);
-        if (!cand) break;
-        cand &= cand - 1u;
-        j = jn;
-        p = pn;
-    }
-#else
     while (cand) {
         const int j = L.j0 + __builtin_ctz(cand);
         cand &= cand - 1u;
         f(j, xy[L.ab + j]);
     }
-#endif
 }
-
-// Candidate list of the contact solver kept across push iterations (SWARM_VERLET).
-struct PairList {
-    uint32_t cand;
-    float bx, by;       // this robot's position when the list was built
-    bool built;         // wave-uniform
-};
 
 // ---------------------------------------------------------------------------
 //  Collisions
@@ -520,8 +491,7 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 // Returns false only when it is known (wave-uniformly) that no pair term
 // contributed, i.e. the push was the identity map on every lane.
 template <int LY, int C>
-__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y,
-                                            PairList* vl = nullptr) {
+__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
     if (SWARM_ABLATE & 4) return false;
     SWARM_WT(L.wt_push++);
     SWARM_PH_T(wt_t);
@@ -532,6 +502,14 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
     auto pair_term = [&](int j, float dx, float dy) {
+#if SWARM_PAIR_RSQ
+        const float s2 = fmaf(dx, dx, fmaf(dy, dy, 1e-8f));
+        const float rs = __builtin_amdgcn_rsqf(s2);
+        const float ov = fmaf(-s2, rs, g.min_dist);      // min_dist - dist
+        if (!(ov > 0.0f)) return;
+        const float hh = ov * rs * 0.5f;
+        const float hx = hh * dx, hy = hh * dy;
+#else
         const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
         const float ov = g.min_dist - dist;
         if (!(ov > 0.0f)) return;
@@ -542,48 +520,18 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         // not branched: the other sums add +0, which leaves them unchanged (a sum
         // that starts at +0 never becomes -0 under round-to-nearest).
         const float hx = ov * nx * 0.5f, hy = ov * ny * 0.5f;
+#endif
         const bool row = j > L.i;
         rx += row ? hx : 0.0f;
         ry += row ? hy : 0.0f;
         cx += row ? 0.0f : -hx;
         cy += row ? 0.0f : -hy;
     };
-    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
-        // compile-time chunk: the C neighbour positions stay in registers and the
-        // exact term runs predicated (skipped by the wave when no lane needs it)
-        float2 p[C];
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) p[jj] = S.xy[L.ab + min(L.j0 + jj, L.N - 1)];
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) {
-            const int j = L.j0 + jj;
-            const float dx = x - p[jj].x, dy = y - p[jj].y;
-            const float s = dx * dx + dy * dy + 1e-8f;
-            if (j < L.j1 && j != L.i && s < g.min_dist2_hi) pair_term(j, dx, dy);
-        }
-    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
-        uint32_t cand;
-        if (SWARM_VERLET && vl) {
-            // rebuild unless every robot of the arena moved less than margin / 2 since
-            // the last build (then |d_ij| changed by less than the margin)
-            const float mx = x - vl->bx, my = y - vl->by;
-            constexpr float h = 0.5f * SWARM_VERLET_MARGIN;
-            if (!vl->built || __any(mx * mx + my * my >= h * h)) {
-                const float vd = g.min_dist + SWARM_VERLET_MARGIN, vd2 = vd * vd * 1.0001f;
-                vl->cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
-                    return dx * dx + dy * dy + 1e-8f < vd2;
-                });
-                vl->bx = x;
-                vl->by = y;
-                vl->built = true;
-            }
-            cand = vl->cand;
-        } else {
-            cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
-                return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
-            });
-        }
+        const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
+            return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
+        });
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
@@ -773,13 +721,12 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     gate_walls<MISSION, ISAAC>(g, x, y);
     constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
     bool fixed = false;                                   // wave-uniform
-    PairList vl{0u, 0.0f, 0.0f, false};
 #pragma unroll
     for (int it = 0; it <= K; ++it) {
         if (fixed && it < K) continue;
         const float bx = x, by = y;
         bool pushed = false;
-        if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y, &vl);
+        if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
         walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
@@ -908,7 +855,12 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         SWARM_WT(L.wt_seg++);
         const int s = __builtin_ctz(near_mask);
         near_mask &= near_mask - 1u;
+#if SWARM_SEG_LDS
+        const float4 sg = S.seg[s];
+        const float ax = sg.x, ay = sg.y, sx = sg.z, sy = sg.w;
+#else
         const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
+#endif
         const float qx = ax - x, qy = ay - y;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -942,17 +894,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
     };
-    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
-        float2 p[C];
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) p[jj] = S.xy[L.ab + min(L.j0 + jj, L.N - 1)];
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) {
-            const int j = L.j0 + jj;
-            const float dx = p[jj].x - x, dy = p[jj].y - y;
-            if (j < L.j1 && j != L.i && dx * dx + dy * dy <= 0.0200f) disc(dx, dy);
-        }
-    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         const uint32_t cand = disc_cand ? *disc_cand
                                         : chunk_mask<C>(L, S.xy, x, y,
                                                         [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
@@ -994,7 +936,7 @@ __device__ __forceinline__ void proximity_aggregate(const Geom& g, const float p
 // ES:299-356
 template <int MISSION>
 __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw, float syw, float lt[8], float& lv,
-                                      float& la) {
+                                      float& la, bool need_agg = true) {
     // Homing and XOR have no light (HMC:18, XOC:18; MC:144): readings are zero (DG:353-362)
     constexpr bool HAS_LIGHT = !(MISSION == HOMING || MISSION == XOR);
     if (!HAS_LIGHT) {
@@ -1020,6 +962,7 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
         sx += raw * g.cos_a[k];
         sy += raw * g.sin_a[k];
     }
+    if (!need_agg) return;   // the cache aggregates are not read in this substep (SWARM_LAST_CACHE)
     const float ang = atan2f(sy, sx);
     const bool above = mx > g.light_thr;
     lv = above ? mx : 0.0f;
@@ -1031,7 +974,8 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
 // neighbour chunk. u_replay: this robot's row of N uniforms, or nullptr
 // (Philox stream `purpose`, one block per 5 neighbours).
 template <int C>
-__device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv, float x,
+__device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv,
+                                            const float4* seg, float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
                                             uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy,
                                             const uint32_t* pre_cand = nullptr, const uint4* pre_rb = nullptr) {
@@ -1050,23 +994,25 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         const bool test_arena = !(me_in && insv[L.ab + j] != 0);
         const int s0 = test_arena ? 0 : 12;
         bool blocked = false;
-#if SWARM_OBS_FUSE
         // no segment to test (convex arena only, both ends strictly inside): skip the divisions
         if (s0 < g.nseg) {
-#endif
         const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
         for (int s = s0; s < g.nseg; ++s) {
+#if SWARM_SEG_LDS
+            const float4 sg = seg[s];
+            const float sx = sg.z, sy = sg.w;
+            const float qx = sg.x - x, qy = sg.y - y;
+#else
             const float sx = g.seg_sx[s], sy = g.seg_sy[s];
             const float qx = g.seg_ax[s] - x, qy = g.seg_ay[s] - y;
+#endif
             const float den = rdx * sy - rdy * sx;
             const float dd = den + 1e-12f;
             const float t = (qx * sy - qy * sx) / dd;
             const float u = (qx * rdy - qy * rdx) / dd;
             blocked |= fabsf(den) > 1e-8f && t > 1e-5f && t < dist - 1e-5f && u >= 0.0f && u <= 1.0f;
         }
-#if SWARM_OBS_FUSE
         }
-#endif
         if (blocked) return;
         n += 1.0f;
         const float du = dist * g.inv_unity;
@@ -1088,37 +1034,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         axx += aw * cb;
         ayy += aw * sb;
     };
-    if constexpr (C > 0 && SWARM_UNROLLED_CHUNKS) {
-        // compile-time chunk: positions in registers; the Philox blocks of the
-        // chunk are drawn once per wave (only if some lane has a candidate)
-        float2 p[C];
-        bool cnd[C];
-        bool anyc = false;
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) {
-            const int j = L.j0 + jj;
-            p[jj] = xy[L.ab + min(j, L.N - 1)];
-            const float dx = p[jj].x - x, dy = p[jj].y - y;
-            const float s = dx * dx + dy * dy + 1e-8f;
-            cnd[jj] = j < L.j1 && j != L.i && s < g.rab_range2_hi;
-            anyc |= cnd[jj];
-        }
-        if (!__any(anyc)) return;
-        uint4 rb = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int jj = 0; jj < C; ++jj) {
-            const int j = L.j0 + jj;
-            float uu;
-            if (u_replay) {
-                uu = cnd[jj] ? u_replay[min(j, L.N - 1)] : 0.0f;
-            } else {
-                if (ChunkRng<C>::fresh(jj))
-                    rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, jj), purpose, tick);
-                uu = ChunkRng<C>::K18 ? u01_of7(rb, jj) : u01_of5(rb, jj % 5);
-            }
-            if (cnd[jj] && uu >= g.rab_loss) term(j, p[jj].x - x, p[jj].y - y);
-        }
-    } else if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18) {
+    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18) {
         // as the K18 path below: every candidate's packet-loss uniform first (one
         // Philox block per chunk), then the term for the kept neighbours in increasing j
         const uint32_t cand = pre_cand ? *pre_cand : chunk_mask<C>(L, xy, x, y, [&](float dx, float dy) {
@@ -1201,8 +1117,9 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
 }
 
 // ES:452-460: ztilde and the four body-frame projections from the sums
-__device__ __forceinline__ void rab_finish(const Geom& g, float n, float wx, float wy, float& zt, float r4[4]) {
-    zt = 1.0f - 2.0f / (1.0f + expf(n));
+__device__ __forceinline__ void rab_finish(const Geom& g, float n, float wx, float wy, float& zt, float r4[4],
+                                           const float* zt_tab = nullptr) {
+    zt = zt_tab ? zt_tab[(int)n] : 1.0f - 2.0f / (1.0f + expf(n));
 #pragma unroll
     for (int k = 0; k < 4; ++k) r4[k] = wx * g.rab_cos[k] + wy * g.rab_sin[k];
 }
@@ -1418,7 +1335,7 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<LY>& S, bool with_
 template <int MISSION, int PROFILE, int LY, int C>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
-                                        float& cyw, const uint4* early_rb = nullptr) {
+                                        float& cyw, bool need_agg = true) {
     SWARM_PH_T(wt_t);
     publish<LY>(g, L, S, x, y);
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
@@ -1431,14 +1348,12 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     }
     float prox[8], lt[8], r4[4], zt;
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
-    constexpr bool FUSE = SWARM_OBS_FUSE && C > 0 && SWARM_BRANCHFREE_CHUNKS && !SWARM_UNROLLED_CHUNKS &&
-                          ChunkRng<C>::K18 && SWARM_ABLATE == 0;
+    constexpr bool FUSE = C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18 && SWARM_ABLATE == 0;
     uint32_t mprox = 0, mrab = 0;
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
         obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
-        if (early_rb) rb = *early_rb;   // drawn at the top of the substep (SWARM_OBS_FUSE == 2)
-        else if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
     }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
@@ -1447,14 +1362,18 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
-        rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
+        rab_partial<C>(g, L, S.xy, S.ins, SEG_LDS_PTR(S), x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
                        FUSE ? &mrab : nullptr, FUSE ? &rb : nullptr);
     SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
-    proximity_aggregate(g, prox, agg.pv, agg.pa);
-    light<MISSION>(g, x, y, cyw, syw, lt, agg.lv, agg.la);
+    if (need_agg) proximity_aggregate(g, prox, agg.pv, agg.pa);
+    light<MISSION>(g, x, y, cyw, syw, lt, agg.lv, agg.la, need_agg);
+#if SWARM_ZT_TABLE
+    rab_finish(g, n, wx, wy, zt, r4, S.zt);
+#else
     rab_finish(g, n, wx, wy, zt, r4);
+#endif
     agg.ax = axx;
     agg.ay = ayy;
     if (L.valid && obs) {
@@ -1491,7 +1410,8 @@ __device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<LY
                                          float cyw, const float* u_replay, uint64_t tick, float& ax, float& ay) {
     publish<LY>(g, L, S, x, y);
     float n, wx, wy;
-    rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax, ay);
+    rab_partial<C>(g, L, S.xy, S.ins, SEG_LDS_PTR(S), x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax,
+                   ay);
     combine<LY, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
 }
 
@@ -1675,16 +1595,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
     const Lane L = make_lane<NA, LY>(gr);
-#if SWARM_PRIO_MODE && SWARM_PRED_PRIO
-    if constexpr (LY == 103) {
-        if (st.cost) {   // one arena per wave: the byte is wave-uniform
-            const int pc = __builtin_amdgcn_readfirstlane((int)st.cost[L.valid ? L.env : 0]);
-            if (pc >= SWARM_PRED_P3) { __builtin_amdgcn_s_setprio(3); L.prio = 3; }
-            else if (pc >= SWARM_PRED_P2) { __builtin_amdgcn_s_setprio(2); L.prio = 2; }
-            else if (pc >= SWARM_PRED_P1) { __builtin_amdgcn_s_setprio(1); L.prio = 1; }
-        }
-    }
-#endif
+    stage_tables<LY>(g, S);
     // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
     const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
     const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
@@ -1741,11 +1652,6 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         const float* u_obs = rp.rab ? rp.rab + ((size_t)s * L.E + (L.valid ? L.env : 0)) * NN + (size_t)L.i * L.N : nullptr;
         TurnSrc ts{rp.turns ? rp.turns + (size_t)s * 3 * EN : nullptr, (size_t)EN, (size_t)q, tick};
 
-        // SWARM_OBS_FUSE == 2: this substep's packet-loss block drawn before the physics, so its
-        // multiply chain overlaps the drive and the contact solver (same counter, same draws)
-        constexpr bool EARLY_RB = SWARM_OBS_FUSE == 2 && !REPLAY && C > 0 && ChunkRng<C>::K18;
-        uint4 rb_obs = make_uint4(0, 0, 0, 0);
-        if constexpr (EARLY_RB) rb_obs = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
         // ------------------------------ actions ------------------------------
         SWARM_PH_T(wt_t);
         float lw, rw;
@@ -1840,8 +1746,10 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw,
-                                         EARLY_RB ? &rb_obs : nullptr);
+        // SWARM_LAST_CACHE: with continuous actions (Isaac profile) the cache aggregates are only
+        // stored at the end of the launch; nothing reads them in between
+        const bool need_agg = !SWARM_LAST_CACHE || DISCRETE || PROFILE == STANDALONE || s == n_sub - 1;
+        observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw, need_agg);
     }
 
     // ---- store state and per-call outputs (wave 0; all waves hold the same values) ----
@@ -1866,9 +1774,6 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             st.comp_rew[L.env] = comp;
             if (out.reward) out.reward[L.env] = rew_acc;
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
-#if SWARM_PRIO_MODE && SWARM_PRED_PRIO
-            if (LY == 103 && st.cost) st.cost[L.env] = (uint8_t)min(L.moved_iters, 255);
-#endif
         }
     }
 #if SWARM_WAVE_TIMING
@@ -1912,6 +1817,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom gr, const DevState
     const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY> S;
     const Lane L = make_lane<NA, LY>(gr);
+    stage_tables<LY>(g, S);
     const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
     const size_t EN = (size_t)L.E * L.N;
     float x = 0.0f, y = 0.0f, yaw = 0.0f;

@@ -137,3 +137,23 @@ def test_categorical_terms(K, mask_kind, with_denom, gpu_device):
     _close(out[0][0], out[1][0], 1e-6, "log_prob")
     _close(out[0][1], out[1][1], 1e-6, "mean entropy")
     _close(out[0][2], out[1][2], 2e-6, "d logits")
+
+
+def test_categorical_terms_flag_out_of_range_actions(gpu_device):
+    """An action outside [0, K) (e.g. a -1 option sentinel), even on a masked-out row, is not a
+    silent NaN: the kernel flags it and check_categorical_actions raises (torch's gather raises
+    on such an index too); valid actions leave the flag clear."""
+    from SwarmACB_isaac.agents._trainer import categorical_terms, check_categorical_actions
+
+    M, K = 256, 6
+    z = torch.randn(M, K, device=gpu_device)
+    acts = torch.randint(0, K, (M,), device=gpu_device)
+    mask = torch.ones(M, dtype=torch.bool, device=gpu_device)
+    categorical_terms(z, acts, mask)
+    check_categorical_actions(gpu_device)                     # clean
+    acts[17] = -1
+    mask[17] = False
+    categorical_terms(z, acts, mask)
+    with pytest.raises(IndexError):
+        check_categorical_actions(gpu_device)
+    check_categorical_actions(gpu_device)                     # the check reset the flag

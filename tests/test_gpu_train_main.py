@@ -72,3 +72,30 @@ def test_train_main_one_update_then_play(name, prefix, tag, tmp_path, gpu_device
     rewards = play.main(["--checkpoint", str(final), "--config", cfg_path, "--num_envs", "2",
                          "--num_episodes", "2", "--seed", "1", "--device", str(gpu_device)])
     assert len(rewards) == 2 and all(math.isfinite(r) for r in rewards)
+
+
+def test_reference_script_paths_train_then_play(tmp_path, gpu_device):
+    """`python scripts/train.py` / `python scripts/play.py` (the reference's paths,
+    scripts/train.py:109-207, scripts/play.py:290) as child processes: one POCA update on
+    Foraging_cyclamen at 64 envs, then the final checkpoint played."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    per_decision = E * 20
+    cfg_path, behavior = _write_config("Foraging_cyclamen.yaml", tmp_path, summary_freq=per_decision)
+    total = (behavior["hyperparameters"]["buffer_size"] // per_decision + 1) * per_decision
+    ckpt_dir = tmp_path / "ckpt"
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "train.py"), "--config", cfg_path,
+                        "--num_envs", str(E), "--total_timesteps", str(total), "--log_dir", str(tmp_path / "runs"),
+                        "--checkpoint_dir", str(ckpt_dir), "--seed", "3", "--headless",
+                        "--device", str(gpu_device)], capture_output=True, text=True, timeout=100, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    final = ckpt_dir / "poca_final.pt"
+    assert int(torch.load(final, map_location="cpu", weights_only=True)["update_count"]) == 1
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "play.py"), "--checkpoint", str(final),
+                        "--config", cfg_path, "--num_envs", "2", "--num_episodes", "2", "--headless",
+                        "--device", str(gpu_device)], capture_output=True, text=True, timeout=100, cwd=root, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
