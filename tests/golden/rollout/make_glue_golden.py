@@ -62,10 +62,13 @@ class ScriptedEnv:
         self.max_episode_length = 1200
         self.rewards = torch.randint(0, 4, (steps, E), generator=g).float()
         tr = torch.zeros(steps, E, dtype=torch.bool)
-        tr[4, 1] = True          # env 1 times out mid-decision (substep 4 of decision 0)
-        tr[7:10, 2] = True       # env 2: several substeps of one decision
+        if E > 1:
+            tr[4, 1] = True      # env 1 times out mid-decision (substep 4 of decision 0)
+        if E > 2:
+            tr[7:10, 2] = True   # env 2: several substeps of one decision
         tr[steps - 1, :] = True  # synchronous episode end on the last substep
-        tr[11, 3] = tr[17, 3] = True
+        if E > 3:
+            tr[11, 3] = tr[17, 3] = True
         self.trunc = tr
         self.group = torch.randn(steps, E, generator=g)
         self.obs = torch.randn(steps + 1, E, N, obs_dim, generator=g)

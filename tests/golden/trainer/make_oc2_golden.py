@@ -103,8 +103,32 @@ STATE_KEYS = ("actor_memory_h", "actor_memory_c", "team_memory_h", "team_memory_
 MODULES = ("actor", "team_critic", "action_critic", "option_critic")
 
 
-def run_case(LOT, name, *, E, N, R, dp, cfg_kw, seed, do_update):
+START_ROW_KEYS = ("memory_h", "memory_c", "team_memory_h", "team_memory_c", "action_baseline_memory_h",
+                  "action_baseline_memory_c", "option_joint_memory_h", "option_joint_memory_c",
+                  "option_baseline_memory_h", "option_baseline_memory_c")
+
+
+def chunk_start_rows(dones, L):
+    """(T, E) mask of the rows get_sequence_batches reads the START_ROW_KEYS memories from:
+    the chunk starts of every episode segment (LOB:237-267)."""
+    T, E = dones.shape
+    L = max(1, min(int(L), T))
+    m = np.zeros((T, E), bool)
+    for e in range(E):
+        start = 0
+        ends = [t + 1 for t in range(T) if dones[t, e] > 0.5]
+        if not ends or ends[-1] != T:
+            ends.append(T)
+        for end in ends:
+            m[start:end:L, e] = True
+            start = end
+    return m
+
+
+def run_case(LOT, name, *, E, N, R, dp, cfg_kw, seed, do_update, extra_truncations=(), start_rows_only=False):
     env = ContinuousCyclamenEnv(E, N, dp * R, seed)
+    for k, e in extra_truncations:          # (substep, env) time-outs added to the script
+        env.trunc[k, e] = True
     cfg = LOT.LearnedOptionCriticConfig(horizon=R, decision_period=dp, log_dir="/tmp/_oc2_runs",
                                         checkpoint_dir="/tmp/_oc2_ckpt", **cfg_kw)
     torch.manual_seed(seed)
@@ -130,6 +154,14 @@ def run_case(LOT, name, *, E, N, R, dp, cfg_kw, seed, do_update):
     out["ptr"] = np.int64(T)
     for k in BUF_KEYS:
         out[f"buf/{k}"] = getattr(b, k)[:T].numpy().copy()
+    if start_rows_only:
+        # the sequence batcher reads these memories only at chunk starts (LOB:237-403): the other rows
+        # are zeroed in the file (they compress away; a trainer that read them would fail the test)
+        keep = chunk_start_rows(out["buf/dones"], cfg_kw["sequence_length"])
+        for k in START_ROW_KEYS:
+            v = out[f"buf/{k}"]
+            v[~keep] = 0.0
+        out["start_rows_only"] = np.int64(1)
     for k in STATE_KEYS:
         out[f"state/{k}"] = getattr(tr, k).numpy().copy()
     out["global_step"] = np.int64(tr.global_step)
@@ -255,6 +287,18 @@ def main(only=()):
                         option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
                         critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=320,
                         target_kl=0.01, num_epochs=1)),
+        # the same networks at the config's sequence length 128 (OC2_XOR_cyclamen.yaml:61): 1 env x 130
+        # decisions, a time-out in decision 1 and at the last one -> chunks [0,2) [2,130): a full-length
+        # sequence whose memories start after an episode end, a 2-step one, zero padding; ONE minibatch
+        # of the 40 sequences. Only the chunk-start rows of the start-read memories are kept in the file
+        # (the actor's next_memory rows, 448 floats per agent, are the bulk of it).
+        "oc2_update_h128_L128": lambda: run_case(
+            LOT, "oc2_update_h128_L128", E=1, N=20, R=130, dp=5, seed=17, do_update=True,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=128,
+                        option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=12800,
+                        target_kl=0.01, num_epochs=1, total_timesteps=10_000_000),
+            extra_truncations=((5 * 1 + 3, 0),), start_rows_only=True),
     }
     for name, fn in cases.items():
         if not only or name in only:

@@ -42,9 +42,11 @@ class DiscreteScriptedEnv(ScriptedEnv):
         self.cfg.num_actions = num_actions
 
 
-def run_case(PT, name, *, discrete, recurrent, E, N, D, R, dp, cfg_kw, seed):
+def run_case(PT, name, *, discrete, recurrent, E, N, D, R, dp, cfg_kw, seed, extra_truncations=()):
     steps = dp * R
     env = (DiscreteScriptedEnv(E, N, D, steps, seed, 6) if discrete else ScriptedEnv(E, N, D, steps, seed))
+    for k, e in extra_truncations:          # (substep, env) time-outs added to the script
+        env.trunc[k, e] = True
     cfg = PT.POCAConfig(horizon=R, decision_period=dp, log_dir="/tmp/_tr_runs", checkpoint_dir="/tmp/_tr_ckpt",
                         recurrent=recurrent, **cfg_kw)
     torch.manual_seed(seed)
@@ -142,6 +144,18 @@ def main(only=()):
             cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
                         critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=160,
                         num_epochs=1), seed=11),
+        # the same networks at the configs' real sequence length 128 (Foraging_cyclamen.yaml:29): 4 envs x
+        # 140 decisions; besides the script's early time-outs (envs 1-3 in decisions 0-3) env 0 also times
+        # out at decision 70, all at the last one -> chunks [0,71) [71,140) | [0,1) [1,129) [129,140) | ...:
+        # full-length, partial and one-step sequences, zero padding, memories taken at chunk starts after
+        # an episode end (PB:240-337); 12 chunks x 20 agents, 100 sequences per minibatch -> 2 optimizer
+        # steps (1 epoch, the partial third minibatch dropped as the reference does); schedules far from
+        # their end so the Adam steps move the parameters
+        "poca_update_rnn_h128_L128": lambda: run_case(
+            PT, "poca_update_rnn_h128_L128", discrete=True, recurrent=True, E=4, N=20, D=4, R=140, dp=5,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=128,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=12800,
+                        num_epochs=1, total_timesteps=10_000_000), seed=13, extra_truncations=((5 * 70 + 2, 0),)),
     }
     for name, fn in cases.items():
         if not only or name in only:

@@ -44,7 +44,14 @@ OC2_CASES["oc2_update_h128"] = dict(hidden_dim=128, num_layers=1, memory_size=12
                                     option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
                                     critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4,
                                     mini_batch_size=320, target_kl=0.01, num_epochs=1)
-UPDATE_CASES = ("oc2_update", "oc2_update_kl", "oc2_update_h128")
+# the same networks at the config's sequence length 128 (one 128-step chunk after an episode end, a
+# 2-step one; only the chunk-start rows of the start-read memories are in the file)
+OC2_CASES["oc2_update_h128_L128"] = dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=128,
+                                         option_hidden_dim=128, option_num_layers=1, option_memory_size=128,
+                                         critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4,
+                                         mini_batch_size=12800, target_kl=0.01, num_epochs=1,
+                                         total_timesteps=10_000_000)
+UPDATE_CASES = ("oc2_update", "oc2_update_kl", "oc2_update_h128", "oc2_update_h128_L128")
 MODULES = ("actor", "team_critic", "action_critic", "option_critic")
 
 

@@ -27,6 +27,13 @@ CASES = {
     "poca_update_rnn_h128": (True, True, 4, 20, 4, dict(mini_batch_size=160, memory_size=128, sequence_length=2,
                                                         num_layers=1, seed=11, hidden_dim=128, critic_hidden_dim=128,
                                                         critic_num_heads=4, num_epochs=1, horizon=4)),
+    # the same networks at the configs' sequence length 128 over 140 decisions with episode ends inside
+    # the horizon (full, partial and one-step chunks; PB:240-337)
+    "poca_update_rnn_h128_L128": (True, True, 4, 20, 4, dict(mini_batch_size=12800, memory_size=128,
+                                                             sequence_length=128, num_layers=1, seed=13,
+                                                             hidden_dim=128, critic_hidden_dim=128,
+                                                             critic_num_heads=4, num_epochs=1, horizon=140,
+                                                             total_timesteps=10_000_000)),
 }
 COMMON = dict(hidden_dim=16, critic_hidden_dim=16, critic_num_layers=1, critic_num_heads=2, lr_schedule="linear",
               eps_schedule="linear", beta_schedule="linear", total_timesteps=2000, reward_strength=1.0, num_epochs=2,
