@@ -133,16 +133,21 @@ def batch_starts(n: int, per_batch: int) -> list[int]:
     return [a for a in range(0, n, per_batch) if not (min(a + per_batch, n) - a < per_batch and n >= per_batch)]
 
 
-def windowed(spec, arrays, order, starts, per_batch, bytes_per_row, *, mode, budget_bytes=256 << 20, **kw):
+def windowed(spec, arrays, order, starts, per_batch, bytes_per_row, *, mode, budget_bytes=256 << 20, extra=None,
+             **kw):
     """Yield one dict per minibatch, gathering several consecutive minibatches per
     launch (at most `budget_bytes` of output per launch). Batches are consecutive
-    slices of `order`, so a window is one contiguous range of it."""
+    slices of `order`, so a window is one contiguous range of it. `extra` = (spec,
+    arrays, chunks): fields gathered by a second launch through another chunk table
+    (chunk-start storage, _base.RolloutStorage)."""
     n = order.numel()
     per_window = max(1, int(budget_bytes // max(1, bytes_per_row * per_batch)))
     for w in range(0, len(starts), per_window):
         group = starts[w:w + per_window]
         lo, hi = group[0], min(group[-1] + per_batch, n)
         big = gather(mode, spec, arrays, order[lo:hi], **kw)
+        if extra is not None:
+            big.update(gather(mode, extra[0], extra[1], order[lo:hi], **dict(kw, chunks=extra[2])))
         sizes = [min(a + per_batch, n) - a for a in group]
         parts = [(k, v.split(sizes)) for k, v in big.items()]  # one view per batch, made in C++
         for j in range(len(group)):

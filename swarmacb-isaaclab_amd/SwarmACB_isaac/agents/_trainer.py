@@ -332,11 +332,32 @@ class TrainerBase:
         self.grad_hook = None
         self.step_hook = None
 
+    def episode_decisions(self) -> int:
+        """Decisions of a whole episode: ceil(max_episode_length / decision_period), the
+        episode_steps_left of train() at an episode start (poca_trainer.py:884-890)."""
+        L = int(getattr(self.unwrapped, "max_episode_length", 0) or 0)
+        return max(1, (L + self.decision_period - 1) // self.decision_period) if L > 0 else int(self.cfg.horizon)
+
     def _buffer_capacity(self) -> int:
-        """horizon + the decisions the ML-Agents trigger may add, counted over ALL ranks
-        (poca_trainer.py:337-340, option_critic_trainer.py:207-210)."""
+        """The rows train() can write before an update, counted over ALL ranks. The reference
+        allocates horizon + ceil(buffer_size / per_decision) + 1 rows (poca_trainer.py:337-340,
+        option_critic_trainer.py:207-210, learned_option_critic_trainer.py:506-509), but its loop
+        (poca_trainer.py:876-912) collects min(horizon, episode_steps_left) decisions per call and
+        stops once buffer_size is exceeded: no call adds more than min(horizon, episode decisions)
+        rows, so the horizon term is capped by the episode length (the same count as the
+        reference whenever horizon <= episode decisions). With time_horizon 1000 and 360-decision
+        episodes (the cyclamen configs) the reference's 1,002 rows would be 2.8x the storage
+        train() can use: at C5 (OC2, 4096 envs x 20 agents per GPU) the difference between
+        fitting in HBM or not."""
         per_decision = self.per_decision
-        return self.cfg.horizon + (self.cfg.buffer_size_hint + per_decision - 1) // per_decision + 1
+        return (min(self.cfg.horizon, self.episode_decisions())
+                + (self.cfg.buffer_size_hint + per_decision - 1) // per_decision + 1)
+
+    def _start_row_layout(self) -> dict:
+        """Buffer kwargs of the chunk-start storage of the recurrent memories
+        (_base.RolloutStorage): the update's sequence length and the episode length."""
+        L = int(getattr(self.cfg, "sequence_length", 0) or 0)
+        return dict(chunk_length=L, episode_decisions=self.episode_decisions()) if L > 0 else {}
 
     def _apply_schedules(self):
         """poca_trainer.py:425-435."""

@@ -156,8 +156,8 @@ class POCARolloutCollector:
             if self.recurrent:
                 # the pre-decision memories go straight into buffer row t (nothing reads the row
                 # before the step, and the networks return new memory tensors)
-                buf.memory_h[t].copy_(self.actor_memory_h.squeeze(0).view(E, N, -1))
-                buf.memory_c[t].copy_(self.actor_memory_c.squeeze(0).view(E, N, -1))
+                buf.put_start("memory_h", t, self.actor_memory_h.squeeze(0).view(E, N, -1))
+                buf.put_start("memory_c", t, self.actor_memory_c.squeeze(0).view(E, N, -1))
                 logits, nm = self.actor.step(flat_obs, (self.actor_memory_h, self.actor_memory_c))
                 self.actor_memory_h, self.actor_memory_c = nm[0].detach(), nm[1].detach()
                 dist = torch.distributions.Categorical(validate_args=False, logits=logits)
@@ -175,10 +175,10 @@ class POCARolloutCollector:
             critic_actions = self._encode_actions_for_critic(all_actions)
             if self.recurrent:
                 if buf.critic_memory_size > 0:
-                    buf.critic_memory_h[t].copy_(self.critic_memory_h.squeeze(0))
-                    buf.critic_memory_c[t].copy_(self.critic_memory_c.squeeze(0))
-                    buf.baseline_memory_h[t].copy_(self.baseline_memory_h.squeeze(0).view(E, N, -1))
-                    buf.baseline_memory_c[t].copy_(self.baseline_memory_c.squeeze(0).view(E, N, -1))
+                    buf.put_start("critic_memory_h", t, self.critic_memory_h.squeeze(0))
+                    buf.put_start("critic_memory_c", t, self.critic_memory_c.squeeze(0))
+                    buf.put_start("baseline_memory_h", t, self.baseline_memory_h.squeeze(0).view(E, N, -1))
+                    buf.put_start("baseline_memory_c", t, self.baseline_memory_c.squeeze(0).view(E, N, -1))
                 (team_val, ncm), (baselines, nbm) = self._value_and_baselines(
                     critic_state, critic_actions, (self.critic_memory_h, self.critic_memory_c),
                     (self.baseline_memory_h, self.baseline_memory_c))

@@ -59,11 +59,18 @@ class LearnedOptionRolloutBuffer(RolloutStorage):
     """Recurrent rollout storage for primitive and option-level objectives."""
 
     _full_message = "Learned Option-Critic rollout buffer is full"
+    START_FIELDS = ("memory_h", "memory_c", "team_memory_h", "team_memory_c", "action_baseline_memory_h",
+                    "action_baseline_memory_c", "option_joint_memory_h", "option_joint_memory_c",
+                    "option_baseline_memory_h", "option_baseline_memory_c")
 
     def __init__(self, horizon: int, num_envs: int, num_agents: int, obs_dim: int, state_dim: int, act_dim: int,
                  memory_size: int, critic_memory_size: int, gamma: float, lam: float,
-                 device: torch.device | str):
+                 device: torch.device | str, chunk_length: int | None = None,
+                 episode_decisions: int | None = None):
+        """chunk_length / episode_decisions (optional): keep the ten start-read memories only at
+        chunk-start rows (_base.RolloutStorage)."""
         self._init_dims(horizon, num_envs, num_agents, gamma, lam, device)
+        self._init_start_rows(chunk_length, episode_decisions)
         self.obs_dim, self.state_dim, self.act_dim = int(obs_dim), int(state_dim), int(act_dim)
         self.memory_size, self.critic_memory_size = int(memory_size), int(critic_memory_size)
         T, E, N, M, H, z = self.horizon, self.num_envs, self.num_agents, self.memory_size, \
@@ -89,20 +96,20 @@ class LearnedOptionRolloutBuffer(RolloutStorage):
         self.action_baselines = z(T, E, N)
         self.joint_option_values = z(T, E)
         self.option_baselines = z(T, E, N)
-        self.memory_h = z(T, E, N, M)
-        self.memory_c = z(T, E, N, M)
+        self.memory_h = self._start_zeros(E, N, M)
+        self.memory_c = self._start_zeros(E, N, M)
         self.next_memory_h = z(T, E, N, M)
         self.next_memory_c = z(T, E, N, M)
-        self.team_memory_h = z(T, E, H)
-        self.team_memory_c = z(T, E, H)
-        self.action_baseline_memory_h = z(T, E, N, H)
-        self.action_baseline_memory_c = z(T, E, N, H)
-        self.option_joint_memory_h = z(T, E, H)
-        self.option_joint_memory_c = z(T, E, H)
+        self.team_memory_h = self._start_zeros(E, H)
+        self.team_memory_c = self._start_zeros(E, H)
+        self.action_baseline_memory_h = self._start_zeros(E, N, H)
+        self.action_baseline_memory_c = self._start_zeros(E, N, H)
+        self.option_joint_memory_h = self._start_zeros(E, H)
+        self.option_joint_memory_c = self._start_zeros(E, H)
         self.next_option_joint_memory_h = z(T, E, H)
         self.next_option_joint_memory_c = z(T, E, H)
-        self.option_baseline_memory_h = z(T, E, N, H)
-        self.option_baseline_memory_c = z(T, E, N, H)
+        self.option_baseline_memory_h = self._start_zeros(E, N, H)
+        self.option_baseline_memory_c = self._start_zeros(E, N, H)
         self.returns = z(T, E)
         self.action_advantages = z(T, E, N)
         self.option_advantages = z(T, E, N)

@@ -190,7 +190,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
             horizon=self._buffer_capacity(), num_envs=self.num_envs, num_agents=self.num_agents,
             obs_dim=self.obs_dim, state_dim=self.state_dim, act_dim=self.act_dim,
             memory_size=self.actor.hidden_size, critic_memory_size=self.team_critic.hidden_size, gamma=cfg.gamma,
-            lam=cfg.lam, device=self.device)
+            lam=cfg.lam, device=self.device, **self._start_row_layout())
         self.collector = LearnedOptionCollector(
             env, self.buffer, self.actor, self.team_critic, self.action_critic, self.option_critic,
             decision_period=self.decision_period, reward_strength=self.reward_strength,

@@ -99,8 +99,8 @@ class FixedOptionCollector:
             if obs.data_ptr() != buf.obs[t].data_ptr():
                 buf.obs[t].copy_(obs)
             flat_obs = buf.obs[t].reshape(E * N, -1)
-            buf.memory_h[t].copy_(self.manager_memory_h.view(E, N, -1))
-            buf.memory_c[t].copy_(self.manager_memory_c.view(E, N, -1))
+            buf.put_start("memory_h", t, self.manager_memory_h.view(E, N, -1))
+            buf.put_start("memory_c", t, self.manager_memory_c.view(E, N, -1))
             option_logits, termination_logits, nm = self.manager.step(
                 flat_obs, (self.manager_memory_h, self.manager_memory_c))
             self.manager_memory_h, self.manager_memory_c = nm[0], nm[1]
@@ -120,12 +120,12 @@ class FixedOptionCollector:
 
             critic_state = self._critic_state(buf.critic_states[t])
             options_1h = torch.nn.functional.one_hot(cur, num_classes=O).float()
-            buf.value_memory_h[t].copy_(self.value_memory_h[0])
-            buf.value_memory_c[t].copy_(self.value_memory_c[0])
-            buf.joint_memory_h[t].copy_(self.joint_memory_h[0])
-            buf.joint_memory_c[t].copy_(self.joint_memory_c[0])
-            buf.baseline_memory_h[t].copy_(self.baseline_memory_h.view(E, N, -1))
-            buf.baseline_memory_c[t].copy_(self.baseline_memory_c.view(E, N, -1))
+            buf.put_start("value_memory_h", t, self.value_memory_h[0])
+            buf.put_start("value_memory_c", t, self.value_memory_c[0])
+            buf.put_start("joint_memory_h", t, self.joint_memory_h[0])
+            buf.put_start("joint_memory_c", t, self.joint_memory_c[0])
+            buf.put_start("baseline_memory_h", t, self.baseline_memory_h.view(E, N, -1))
+            buf.put_start("baseline_memory_c", t, self.baseline_memory_c.view(E, N, -1))
             (team_value, nvm), (joint, njm), (baselines, nbm) = self._value_joint_baselines(critic_state, options_1h)
             self.value_memory_h, self.value_memory_c = nvm[0], nvm[1]
             self.joint_memory_h, self.joint_memory_c = njm[0], njm[1]
@@ -241,8 +241,8 @@ class LearnedOptionCollector:
             if obs.data_ptr() != buf.obs[t].data_ptr():
                 buf.obs[t].copy_(obs)
             flat_obs = buf.obs[t].reshape(E * N, -1)
-            buf.memory_h[t].copy_(self.actor_memory_h.view(E, N, -1))
-            buf.memory_c[t].copy_(self.actor_memory_c.view(E, N, -1))
+            buf.put_start("memory_h", t, self.actor_memory_h.view(E, N, -1))
+            buf.put_start("memory_c", t, self.actor_memory_c.view(E, N, -1))
             (_sel, option_values, termination_logits, action_means, action_stds, _att,
              nm) = self.actor.step(flat_obs, (self.actor_memory_h, self.actor_memory_c))
             self.actor_memory_h, self.actor_memory_c = nm[0], nm[1]
@@ -273,14 +273,14 @@ class LearnedOptionCollector:
             critic_state = self._critic_state(buf.critic_states[t])
             options_1h = torch.nn.functional.one_hot(cur, num_classes=O).float()
             option_states = torch.cat([critic_state, options_1h], dim=-1)
-            buf.team_memory_h[t].copy_(self.team_memory_h[0])
-            buf.team_memory_c[t].copy_(self.team_memory_c[0])
-            buf.action_baseline_memory_h[t].copy_(self.action_baseline_memory_h.view(E, N, -1))
-            buf.action_baseline_memory_c[t].copy_(self.action_baseline_memory_c.view(E, N, -1))
-            buf.option_joint_memory_h[t].copy_(self.option_joint_memory_h[0])
-            buf.option_joint_memory_c[t].copy_(self.option_joint_memory_c[0])
-            buf.option_baseline_memory_h[t].copy_(self.option_baseline_memory_h.view(E, N, -1))
-            buf.option_baseline_memory_c[t].copy_(self.option_baseline_memory_c.view(E, N, -1))
+            buf.put_start("team_memory_h", t, self.team_memory_h[0])
+            buf.put_start("team_memory_c", t, self.team_memory_c[0])
+            buf.put_start("action_baseline_memory_h", t, self.action_baseline_memory_h.view(E, N, -1))
+            buf.put_start("action_baseline_memory_c", t, self.action_baseline_memory_c.view(E, N, -1))
+            buf.put_start("option_joint_memory_h", t, self.option_joint_memory_h[0])
+            buf.put_start("option_joint_memory_c", t, self.option_joint_memory_c[0])
+            buf.put_start("option_baseline_memory_h", t, self.option_baseline_memory_h.view(E, N, -1))
+            buf.put_start("option_baseline_memory_c", t, self.option_baseline_memory_c.view(E, N, -1))
             (team_value, ntm), _, _ = self.team_critic.decision_passes(
                 critic_state, None, value=True, joint=False, baselines=False,
                 value_memory=(self.team_memory_h, self.team_memory_c))

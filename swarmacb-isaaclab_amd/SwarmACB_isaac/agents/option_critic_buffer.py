@@ -48,11 +48,17 @@ class FixedOptionRolloutBuffer(RolloutStorage):
     """(T, E, N, ...) storage for the fixed-option trainer; team quantities are (T, E)."""
 
     _full_message = "Fixed Option-Critic rollout buffer is full"
+    START_FIELDS = ("memory_h", "memory_c", "value_memory_h", "value_memory_c", "joint_memory_h", "joint_memory_c",
+                    "baseline_memory_h", "baseline_memory_c")
 
     def __init__(self, horizon: int, num_envs: int, num_agents: int, obs_dim: int, state_dim: int,
                  memory_size: int, critic_memory_size: int, gamma: float, lam: float,
-                 device: torch.device | str):
+                 device: torch.device | str, chunk_length: int | None = None,
+                 episode_decisions: int | None = None):
+        """chunk_length / episode_decisions (optional): keep the start-read memories only at
+        chunk-start rows (_base.RolloutStorage)."""
         self._init_dims(horizon, num_envs, num_agents, gamma, lam, device)
+        self._init_start_rows(chunk_length, episode_decisions)
         self.gamma, self.lam = gamma, lam
         self.obs_dim, self.state_dim = obs_dim, state_dim
         self.memory_size, self.critic_memory_size = memory_size, critic_memory_size
@@ -72,18 +78,18 @@ class FixedOptionRolloutBuffer(RolloutStorage):
         self.team_values = z(T, E)
         self.joint_option_values = z(T, E)
         self.baselines = z(T, E, N)
-        self.memory_h = z(T, E, N, memory_size)
-        self.memory_c = z(T, E, N, memory_size)
+        self.memory_h = self._start_zeros(E, N, memory_size)
+        self.memory_c = self._start_zeros(E, N, memory_size)
         self.next_memory_h = z(T, E, N, memory_size)
         self.next_memory_c = z(T, E, N, memory_size)
-        self.value_memory_h = z(T, E, H)
-        self.value_memory_c = z(T, E, H)
-        self.joint_memory_h = z(T, E, H)
-        self.joint_memory_c = z(T, E, H)
+        self.value_memory_h = self._start_zeros(E, H)
+        self.value_memory_c = self._start_zeros(E, H)
+        self.joint_memory_h = self._start_zeros(E, H)
+        self.joint_memory_c = self._start_zeros(E, H)
         self.next_joint_memory_h = z(T, E, H)
         self.next_joint_memory_c = z(T, E, H)
-        self.baseline_memory_h = z(T, E, N, H)
-        self.baseline_memory_c = z(T, E, N, H)
+        self.baseline_memory_h = self._start_zeros(E, N, H)
+        self.baseline_memory_c = self._start_zeros(E, N, H)
         self.returns = z(T, E)
         self.advantages = z(T, E, N)
 

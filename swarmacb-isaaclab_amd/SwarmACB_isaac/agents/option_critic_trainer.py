@@ -78,7 +78,8 @@ class FixedOptionCriticTrainer(TrainerBase):
         self.buffer = FixedOptionRolloutBuffer(
             horizon=self._buffer_capacity(), num_envs=self.num_envs, num_agents=self.num_agents,
             obs_dim=self.obs_dim, state_dim=self.state_dim, memory_size=self.manager.hidden_size,
-            critic_memory_size=self.critic.hidden_size, gamma=c.gamma, lam=c.lam, device=self.device)
+            critic_memory_size=self.critic.hidden_size, gamma=c.gamma, lam=c.lam, device=self.device,
+            **self._start_row_layout())
         self.collector = FixedOptionCollector(env, self.buffer, self.manager, self.critic,
                                               decision_period=self.decision_period,
                                               reward_strength=self.reward_strength, num_options=c.num_options)

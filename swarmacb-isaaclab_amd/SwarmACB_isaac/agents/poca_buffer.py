@@ -49,11 +49,18 @@ class POCARolloutBuffer(RolloutStorage):
     """Fixed-horizon storage for POCA; tensors are (T, E, ...)."""
 
     _full_message = "POCA rollout buffer is full"
+    START_FIELDS = ("memory_h", "memory_c", "critic_memory_h", "critic_memory_c", "baseline_memory_h",
+                    "baseline_memory_c")
 
     def __init__(self, horizon: int, num_envs: int, num_agents: int, obs_dim: int, act_dim: int,
                  state_dim: int = 5, memory_size: int = 0, critic_memory_size: int = 0, gamma: float = 0.99,
-                 lam: float = 0.95, device: torch.device | str = "cuda"):
+                 lam: float = 0.95, device: torch.device | str = "cuda", chunk_length: int | None = None,
+                 episode_decisions: int | None = None):
+        """chunk_length / episode_decisions (optional): keep the memories only at chunk-start
+        rows (_base.RolloutStorage) for sequence batches of that length."""
         self._init_dims(horizon, num_envs, num_agents, gamma, lam, device)
+        if memory_size:
+            self._init_start_rows(chunk_length, episode_decisions)
         self.gamma, self.lam = gamma, lam
         self.obs_dim, self.act_dim, self.state_dim = obs_dim, act_dim, state_dim
         self.memory_size = int(memory_size or 0)
@@ -70,16 +77,16 @@ class POCARolloutBuffer(RolloutStorage):
         self.team_values = z(T, E)
         self.baselines = z(T, E, N)
         if self.memory_size > 0:
-            self.memory_h = z(T, E, N, self.memory_size)
-            self.memory_c = z(T, E, N, self.memory_size)
+            self.memory_h = self._start_zeros(E, N, self.memory_size)
+            self.memory_c = self._start_zeros(E, N, self.memory_size)
         else:
             self.memory_h = self.memory_c = None
         if self.critic_memory_size > 0:
             H = self.critic_memory_size
-            self.critic_memory_h = z(T, E, H)
-            self.critic_memory_c = z(T, E, H)
-            self.baseline_memory_h = z(T, E, N, H)
-            self.baseline_memory_c = z(T, E, N, H)
+            self.critic_memory_h = self._start_zeros(E, H)
+            self.critic_memory_c = self._start_zeros(E, H)
+            self.baseline_memory_h = self._start_zeros(E, N, H)
+            self.baseline_memory_c = self._start_zeros(E, N, H)
         else:
             self.critic_memory_h = self.critic_memory_c = None
             self.baseline_memory_h = self.baseline_memory_c = None

@@ -88,7 +88,7 @@ class POCATrainer(TrainerBase):
             obs_dim=self.obs_dim, act_dim=self.act_dim, state_dim=self.state_dim,
             memory_size=self.actor.hidden_size if self.recurrent else 0,
             critic_memory_size=self.critic.hidden_size if self.recurrent else 0,
-            gamma=c.gamma, lam=c.lam, device=self.device)
+            gamma=c.gamma, lam=c.lam, device=self.device, **(self._start_row_layout() if self.recurrent else {}))
         self.collector = POCARolloutCollector(
             env, self.buffer, self.actor, self.critic, decision_period=self.decision_period,
             reward_strength=self.reward_strength, discrete=self.discrete, num_actions=self.num_actions,

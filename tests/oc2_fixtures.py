@@ -76,10 +76,7 @@ def make_oc2_trainer(name, device, fused_optimizer=False):
 
 def load_buffer(tr, fx):
     T = int(fx["ptr"])
-    for key in fx.files:
-        if key.startswith("buf/"):
-            getattr(tr.buffer, key[4:])[:T].copy_(torch.as_tensor(fx[key]))
-    tr.buffer.ptr = T
+    tr.buffer.load_rows({key[4:]: fx[key] for key in fx.files if key.startswith("buf/")}, T)
     tr.global_step = int(fx["global_step"])
     with torch.no_grad():
         for m in ("team_critic", "action_critic", "option_critic"):

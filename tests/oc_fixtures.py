@@ -124,10 +124,7 @@ def make_oc_trainer(name, device, env=None):
 def load_buffer(tr, fx):
     T = int(fx["ptr"])
     b = tr.buffer
-    for key in fx.files:
-        if key.startswith("buf/"):
-            getattr(b, key[4:])[:T].copy_(torch.as_tensor(fx[key]))
-    b.ptr = T
+    b.load_rows({key[4:]: fx[key] for key in fx.files if key.startswith("buf/")}, T)
     tr.global_step = int(fx["global_step"])
     with torch.no_grad():
         tr.critic._current_max_agents.copy_(torch.as_tensor(fx["critic_max_agents_after_collect"]))

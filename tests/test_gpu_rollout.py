@@ -215,3 +215,49 @@ def test_edge_cases(gpu_device):
     cpu.ptr = 2
     with pytest.raises(RuntimeError, match="GPU"):
         cpu.compute_returns_and_advantages(torch.zeros(2))
+
+
+@pytest.mark.parametrize("cls", ["poca", "oc2"])
+def test_chunk_start_storage_batches_equal_plain_layout(cls, gpu_device):
+    """A buffer keeping its recurrent memories only at chunk-start rows (_base.RolloutStorage,
+    chunk_length / episode_decisions) yields the same sequence minibatches, field for field and
+    bit for bit, as the plain (T, E, ...) layout fed the same rollout (rows written in order,
+    episode ends inside and across the 16-row windows)."""
+    from SwarmACB_isaac.agents.learned_option_critic_buffer import LearnedOptionRolloutBuffer
+
+    T, E, N, L = 70, 6, 3, 16
+    if cls == "poca":
+        mk = lambda **kw: POCARolloutBuffer(T, E, N, obs_dim=4, act_dim=1, memory_size=8, critic_memory_size=8,  # noqa: E731
+                                            device=gpu_device, **kw)
+    else:
+        mk = lambda **kw: LearnedOptionRolloutBuffer(T, E, N, obs_dim=24, state_dim=5, act_dim=2, memory_size=12,  # noqa: E731
+                                                     critic_memory_size=8, gamma=0.99, lam=0.95, device=gpu_device,
+                                                     **kw)
+    plain, compact = mk(), mk(chunk_length=L, episode_decisions=25)
+    assert compact.compact_starts and not plain.compact_starts
+    gen = torch.Generator(device=gpu_device).manual_seed(5)
+    d = torch.zeros(T, E, device=gpu_device)
+    d[10, 0] = d[24, 1] = d[25, 1] = d[3, 2] = d[40, 2] = d[0, 3] = d[T - 1] = 1
+    for t in range(T):
+        for name in plain.START_FIELDS:
+            v = torch.randn(getattr(plain, name).shape[1:], generator=gen, device=gpu_device)
+            plain.put_start(name, t, v)
+            compact.put_start(name, t, v)
+        plain.dones[t] = compact.dones[t] = d[t]
+    for b in (plain, compact):
+        b.ptr = T
+    for name in ("obs", "critic_states", "actions", "advantages", "returns", "team_values"):
+        src = getattr(plain, name, None)
+        if src is not None:
+            v = torch.randn(src.shape, generator=gen, device=gpu_device)
+            src.copy_(v)
+            getattr(compact, name).copy_(v)
+    torch.manual_seed(11)
+    a = list(plain.get_sequence_batches(L, 5 * L))
+    torch.manual_seed(11)
+    b = list(compact.get_sequence_batches(L, 5 * L))
+    assert len(a) == len(b) > 1
+    for k, (x, y) in enumerate(zip(a, b)):
+        assert set(x) == set(y)
+        for key in x:
+            torch.testing.assert_close(x[key], y[key], rtol=0, atol=0, msg=f"batch {k} {key}")

@@ -37,6 +37,12 @@ def test_buffer_capacity_and_trigger_follow_reference():
     tr = POCATrainer(env, POCAConfig(horizon=7, buffer_size_hint=50, hidden_dim=8, critic_hidden_dim=8,
                                      critic_num_heads=2, log_dir="/tmp/_poca_cap"), writer=TF_null())
     assert tr.buffer.horizon == 7 + (50 + 23) // 24 + 1
+    # a horizon beyond the episode (time_horizon 1000 vs 360-decision episodes in the cyclamen
+    # configs) is capped by the episode length: train() never collects more per call
+    env.max_episode_length = 40                      # 8 decisions of 5 steps
+    tr = POCATrainer(env, POCAConfig(horizon=1000, buffer_size_hint=50, hidden_dim=8, critic_hidden_dim=8,
+                                     critic_num_heads=2, log_dir="/tmp/_poca_cap"), writer=TF_null())
+    assert tr.buffer.horizon == 8 + (50 + 23) // 24 + 1
 
 
 def TF_null():

@@ -84,11 +84,7 @@ def make_trainer(name, device, writer=None):
         tr.critic._current_max_agents.copy_(torch.as_tensor(fx["critic_max_agents_after_collect"]))
     T = int(fx["ptr"])
     b = tr.buffer
-    for key in fx.files:
-        if key.startswith("buf/"):
-            attr = key[4:]
-            getattr(b, attr)[:T].copy_(torch.as_tensor(fx[key]))
-    b.ptr = T
+    b.load_rows({key[4:]: fx[key] for key in fx.files if key.startswith("buf/")}, T)
     tr.global_step = int(fx["global_step"])
     return tr, fx, names, [named[k] for k in names]
 
