@@ -402,10 +402,64 @@ class TrainerBase:
         return (_graph.ENABLED and self.device.type == "cuda" and dist_ok
                 and self.grad_hook is None and self.step_hook is None)
 
+    def eager_reason(self) -> str | None:
+        """Why this rank's optimizer steps run eagerly (None: they are graphed)."""
+        if not _graph.ENABLED:
+            return "SWARM_GRAPHS=0"
+        if self.device.type != "cuda":
+            return "not a GPU device"
+        if self.comm.active and self.comm.backend != "nccl":
+            return f"{self.comm.backend} backend (host round trips cannot be captured)"
+        if self.comm.active and not _graph.DIST_ENABLED:
+            return "multi-rank with SWARM_GRAPHS_DIST=0"
+        if self.grad_hook is not None or self.step_hook is not None:
+            return "per-step test hooks"
+        g = getattr(self, "_graphed", None)
+        if g is not None and g.failed:
+            return "capture failed (see the warning)"
+        return None
+
+    def step_path(self) -> dict:
+        """How this rank ran its optimizer steps so far: graphed replays, eager steps (warm-up,
+        ragged minibatches, or all of them), the reason when they are not graphed, and the mean
+        wall time per optimizer step of the updates (update seconds / steps)."""
+        g = getattr(self, "_graphed", None)
+        replays = g.replays if g is not None else 0
+        steps = getattr(self, "_opt_steps", 0)
+        secs = getattr(self, "_update_seconds", 0.0)
+        return {"rank": self.comm.rank, "world": self.comm.world, "backend": self.comm.backend,
+                "optimizer_steps": steps, "graphed_replays": replays, "eager_steps": steps - replays,
+                "graphed": self.eager_reason() is None and replays > 0, "eager_reason": self.eager_reason(),
+                "ms_per_optimizer_step": 1e3 * secs / steps if steps else None}
+
+    def report_step_path(self, prefix: str = "") -> dict:
+        """Print this rank's step path (every rank prints; the rank is in the line) and log it."""
+        sp = self.step_path()
+        ms = sp["ms_per_optimizer_step"]
+        print(f"[{self.algo}] {prefix}rank {sp['rank']}/{sp['world']} ({sp['backend'] or 'single process'}): "
+              f"optimizer steps {sp['optimizer_steps']}, graphed replays {sp['graphed_replays']}, eager "
+              f"{sp['eager_steps']}" + (f" [{sp['eager_reason']}]" if sp["eager_reason"] else "")
+              + (f", {ms:.3f} ms per step" if ms is not None else ""), flush=True)
+        w = self.writer
+        w.add_scalar("Perf/Optimizer Steps Graphed Fraction",
+                     sp["graphed_replays"] / max(1, sp["optimizer_steps"]), self.global_step)
+        if ms is not None:
+            w.add_scalar("Perf/Optimizer Step ms", ms, self.global_step)
+        return sp
+
     def _step_runner(self, step_fn, optimizers):
         """A callable batch -> detached loss terms: GraphedStep over step_fn when graphs
         are usable, else step_fn itself. The runner (and its graph) persists across updates;
-        it recaptures when the key (schedule values) changes."""
+        it recaptures when the key (schedule values) changes. Every call is counted
+        (step_path)."""
+        inner = self._step_runner_inner(step_fn, optimizers)
+
+        def run(batch, key=None):
+            self._opt_steps = getattr(self, "_opt_steps", 0) + 1
+            return inner(batch, key)
+        return run
+
+    def _step_runner_inner(self, step_fn, optimizers):
         if not self._graphs_ok():
             return lambda batch, key=None: step_fn(batch)
         if getattr(self, "_graphed", None) is None:
@@ -491,7 +545,10 @@ class TrainerBase:
             obs_dict = self._rollout_until_trigger(obs_dict)
             t_update = time.perf_counter()
             metrics = self.update()
+            self._update_seconds = getattr(self, "_update_seconds", 0.0) + time.perf_counter() - t_update
             self._post_update(metrics, time.perf_counter() - t_update, self.global_step - prev_step)
+            if self.update_count == 1:          # which path the optimizer steps took, every rank
+                self.report_step_path("first update: ")
             self._drain_episodes()
             elapsed = time.time() - start_time
             sps = (self.global_step - start_step) / elapsed if elapsed > 0 else 0.0
@@ -514,6 +571,7 @@ class TrainerBase:
             pbar.close()
         # every rank must end with rank 0's parameters (one global update per step)
         self.comm.assert_replicated(self.params, "parameters after training")
+        self.report_step_path("end of training: ")
         if self.comm.active:
             d = self.comm._digest(self.params).tolist()
             print(f"[{self.algo}] rank {self.comm.rank}/{self.comm.world}: envs {self.num_envs} of "

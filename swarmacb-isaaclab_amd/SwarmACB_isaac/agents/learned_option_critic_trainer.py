@@ -739,6 +739,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
                                       + [actor_loss.detach().double(), critic_loss.detach().double()]
                                       + [terms[n].detach().reshape(()).double() for n in OBJECTIVE_NAMES[2:]])
                 num_batches += 1
+                self._opt_steps = getattr(self, "_opt_steps", 0) + 1     # eager step (step_path)
         if actor_updates == 0:
             raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
                                "should guarantee at least one safe policy minibatch.")
