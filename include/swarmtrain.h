@@ -178,6 +178,35 @@ int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logi
                                          const uint8_t* mask_u8, const float* used_denom, const float* g_log_probs,
                                          const float* g_mean_entropy, float* d_logits, void* stream);
 
+/* The learned-option (OC2) update's termination, option-selection and attention terms (agents/
+ * learned_option_critic_trainer.py:1050-1093, 1140-1169, 1282-1322, 956-997; csrc/swarm_oc2terms.hip
+ * states every formula). Each forward is one workgroup writing device scalars (denominators: the
+ * given device scalar, or the local active count clamped to >= 1; the one used is returned for the
+ * backward); each backward is elementwise and reads its incoming gradients from a device array.
+ *   termination: out[8] = loss, prior loss, entropy, mean beta, mean advantage, mean signal, low /
+ *     high saturation over M rows of logits / advantages / term_mask (f32); grads[3] = d/d out[0..2];
+ *   option terms (epsilon-greedy manager, forward only): out[5] = sum log_prob, option entropy,
+ *     marginal entropy, balance, effective options, over M rows of O <= 16 option values; low =
+ *     fp32(eps / O), greedy_add = fp32(1 - eps), log_num_options = fp32 log(O);
+ *   attention: out[3] = diversity, temporal, mean attention over (B, L, O <= 8, D <= 64) weights;
+ *     used_denoms[2] = the row and pair denominators; grads[2] = d/d out[0..1]. */
+int32_t swarm_oc2_termination_terms(int64_t M, const float* logits, const float* advantages, const float* term_mask,
+                                    const float* denom, float penalty, float prior_probability, float* out,
+                                    float* used_denom, void* stream);
+int32_t swarm_oc2_termination_terms_backward(int64_t M, const float* logits, const float* advantages,
+                                             const float* term_mask, const float* used_denom, float penalty,
+                                             float prior_probability, const float* grads, float* d_logits,
+                                             void* stream);
+int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values, const int64_t* options,
+                               const uint8_t* loss_mask, const uint8_t* boundary, const float* boundary_denom,
+                               float low, float greedy_add, float log_num_options, float* out, void* stream);
+int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
+                                  const uint8_t* loss_mask, const float* dones, const float* row_denom,
+                                  const float* pair_denom, float* out, float* used_denoms, void* stream);
+int32_t swarm_oc2_attention_terms_backward(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
+                                           const uint8_t* loss_mask, const float* dones, const float* used_denoms,
+                                           const float* grads, float* d_attentions, void* stream);
+
 /* Copy n tensors of 32-bit words: dst_ptrs[k] <- src_ptrs[k], words[k] words each (all three are
  * DEVICE arrays of n entries, so a captured graph can replay the call; max_words >= every words[k]
  * sizes the grid), skipped entirely when `unless` (a device byte, or NULL = never) is non-zero.

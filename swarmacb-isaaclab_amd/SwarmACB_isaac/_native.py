@@ -75,7 +75,9 @@ TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa
                  "swarm_set_pool_forward", "swarm_set_pool_backward", "swarm_splitk_colsum",
                  "swarm_splitk_finish", "swarm_ppo_value_loss", "swarm_ppo_value_loss_backward",
                  "swarm_ppo_policy_loss", "swarm_ppo_policy_loss_backward", "swarm_categorical_terms",
-                 "swarm_categorical_terms_backward"]
+                 "swarm_categorical_terms_backward", "swarm_oc2_termination_terms",
+                 "swarm_oc2_termination_terms_backward", "swarm_oc2_option_terms", "swarm_oc2_attention_terms",
+                 "swarm_oc2_attention_terms_backward"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 
@@ -202,6 +204,16 @@ def load() -> C.CDLL:
     lib.swarm_ppo_policy_loss_backward.argtypes = [i64, i32, i32, vp, vp, vp, vp, vp, f32, f32, i32, vp, vp, vp, vp]
     lib.swarm_categorical_terms.restype = i32
     lib.swarm_categorical_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.swarm_oc2_termination_terms.restype = i32
+    lib.swarm_oc2_termination_terms.argtypes = [i64, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
+    lib.swarm_oc2_termination_terms_backward.restype = i32
+    lib.swarm_oc2_termination_terms_backward.argtypes = [i64, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
+    lib.swarm_oc2_option_terms.restype = i32
+    lib.swarm_oc2_option_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, vp, vp]
+    lib.swarm_oc2_attention_terms.restype = i32
+    lib.swarm_oc2_attention_terms.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.swarm_oc2_attention_terms_backward.restype = i32
+    lib.swarm_oc2_attention_terms_backward.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_categorical_terms_backward.restype = i32
     lib.swarm_categorical_terms_backward.argtypes = [i64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     if lib.swarm_abi_version() != ABI_VERSION:

@@ -29,6 +29,8 @@ from __future__ import annotations
 
 import copy
 import ctypes as C
+import math
+import os
 import time
 
 import torch
@@ -79,6 +81,131 @@ def stable_trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilo
         active = active.unsqueeze(-1)
     active = active.expand_as(loss)
     return (loss * active).sum() / (denom if denom is not None else active.sum().clamp_min(1.0))
+
+
+# SWARM_FUSED_OC2_TERMS=0: the termination / option-selection / attention terms run as torch ops
+FUSED_OC2_TERMS = os.environ.get("SWARM_FUSED_OC2_TERMS", "1") != "0"
+
+
+def _vp(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(t):
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _scalar_denom(d):
+    """A device scalar denominator for the term kernels, None (local count), or False (unusable)."""
+    if d is None:
+        return None
+    if torch.is_tensor(d) and d.numel() == 1 and d.is_cuda:
+        return d.reshape(()).to(torch.float32).contiguous()
+    return False
+
+
+class _TerminationTerms(torch.autograd.Function):
+    """The termination group of the OC2 losses on swarm_oc2_termination_terms / _backward
+    (include/swarmtrain.h): logits (M,) -> out (8,) = termination loss, prior loss, termination
+    entropy, mean beta, mean advantage, mean signal, low / high saturation."""
+
+    @staticmethod
+    def forward(ctx, logits, adv, term_mask, denom, penalty: float, prior_p: float):
+        z = logits.contiguous()
+        out = torch.empty(8, dtype=z.dtype, device=z.device)
+        used = torch.empty((), dtype=z.dtype, device=z.device)
+        _native.check(_native.load().swarm_oc2_termination_terms(
+            z.numel(), _vp(z), _vp(adv), _vp(term_mask), _vp(denom), penalty, prior_p, _vp(out), _vp(used),
+            _stream(z)), "swarm_oc2_termination_terms")
+        ctx.save_for_backward(z, adv, term_mask, used)
+        ctx.consts = (penalty, prior_p)
+        ctx.shape = logits.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        z, adv, term_mask, used = ctx.saved_tensors
+        penalty, prior_p = ctx.consts
+        g = d_out[:3].contiguous()
+        dz = torch.empty_like(z)
+        _native.check(_native.load().swarm_oc2_termination_terms_backward(
+            z.numel(), _vp(z), _vp(adv), _vp(term_mask), _vp(used), penalty, prior_p, _vp(g), _vp(dz), _stream(z)),
+            "swarm_oc2_termination_terms_backward")
+        return dz.view(ctx.shape), None, None, None, None, None
+
+
+class _AttentionTerms(torch.autograd.Function):
+    """The attention group of the OC2 losses on swarm_oc2_attention_terms / _backward:
+    attentions (B, L, O, D) -> out (3,) = diversity, temporal, mean attention."""
+
+    @staticmethod
+    def forward(ctx, att, mask_u8, dones, d_rows, d_pairs):
+        a = att.contiguous()
+        B, L, O, D = a.shape
+        out = torch.empty(3, dtype=a.dtype, device=a.device)
+        used = torch.empty(2, dtype=a.dtype, device=a.device)
+        _native.check(_native.load().swarm_oc2_attention_terms(
+            B, L, O, D, _vp(a), _vp(mask_u8), _vp(dones), _vp(d_rows), _vp(d_pairs), _vp(out), _vp(used),
+            _stream(a)), "swarm_oc2_attention_terms")
+        ctx.save_for_backward(a, mask_u8, dones, used)
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        a, mask_u8, dones, used = ctx.saved_tensors
+        B, L, O, D = a.shape
+        g = d_out[:2].contiguous()
+        da = torch.empty_like(a)
+        _native.check(_native.load().swarm_oc2_attention_terms_backward(
+            B, L, O, D, _vp(a), _vp(mask_u8), _vp(dones), _vp(used), _vp(g), _vp(da), _stream(a)),
+            "swarm_oc2_attention_terms_backward")
+        return da, None, None, None, None
+
+
+def fused_termination_terms(next_beta_logits, termination_advantage, penalty, prior_p, term_mask, denom):
+    """(termination loss, prior loss, entropy, mean beta, mean advantage, mean signal, low, high) of
+    LOT:1282-1322 in one kernel each way, or None when the inputs do not fit it."""
+    d = _scalar_denom(denom)
+    if not (FUSED_OC2_TERMS and next_beta_logits.is_cuda and next_beta_logits.dtype == torch.float32
+            and d is not False and next_beta_logits.numel() > 0):
+        return None
+    adv = termination_advantage.detach().to(torch.float32).contiguous()
+    w = term_mask.to(torch.float32).contiguous()
+    out = _TerminationTerms.apply(next_beta_logits, adv, w, d, float(penalty), float(prior_p))
+    return tuple(out[k] for k in range(8))
+
+
+def fused_attention_terms(attentions, loss_mask, dones, d_rows, d_pairs):
+    """(diversity, temporal, mean attention) of LOT:956-997 in one kernel each way, or None."""
+    dr, dp = _scalar_denom(d_rows), _scalar_denom(d_pairs)
+    if not (FUSED_OC2_TERMS and attentions.is_cuda and attentions.dtype == torch.float32 and attentions.dim() == 4
+            and 2 <= attentions.shape[2] <= 8 and attentions.shape[3] <= 64 and dr is not False and dp is not False
+            and attentions.numel() > 0):
+        return None
+    m = loss_mask.to(torch.bool).contiguous().view(torch.uint8)
+    out = _AttentionTerms.apply(attentions, m, dones.to(torch.float32).contiguous(), dr, dp)
+    return out[0], out[1], out[2]
+
+
+def fused_option_terms(actor, option_values, options, loss_mask, boundary, epsilon: float, n_bound_denom):
+    """(sum log_prob, option entropy, marginal entropy, balance, effective options) of the
+    epsilon-greedy manager (LOT:1050-1093; no gradient reaches option_values through them) in
+    one kernel, or None."""
+    d = _scalar_denom(n_bound_denom)
+    O = option_values.shape[-1]
+    if not (FUSED_OC2_TERMS and getattr(actor, "epsilon_greedy_selector", False) and option_values.is_cuda
+            and option_values.dtype == torch.float32 and O <= 16 and d is not False and options.numel() > 0
+            and 0.0 <= float(epsilon) <= 1.0):
+        return None
+    q = option_values.detach().reshape(-1, O).contiguous()
+    M = q.shape[0]
+    out = torch.empty(5, dtype=torch.float32, device=q.device)
+    _native.check(_native.load().swarm_oc2_option_terms(
+        M, O, _vp(q), _vp(options.reshape(-1).long().contiguous()),
+        _vp(loss_mask.reshape(-1).to(torch.bool).contiguous().view(torch.uint8)),
+        _vp(boundary.reshape(-1).to(torch.bool).contiguous().view(torch.uint8)), _vp(d),
+        float(epsilon) / O, 1.0 - float(epsilon), math.log(O), _vp(out), _stream(q)), "swarm_oc2_option_terms")
+    return tuple(out[k] for k in range(5))
 
 
 _OFFDIAG = {}
@@ -365,17 +492,23 @@ class LearnedOptionCriticTrainer(TrainerBase):
         ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes(critic_requests)
 
         # AOC: the manager is epsilon-soft over Q_Omega; no selector gradient (LOT:1050-1093)
-        option_dist = self.actor.option_dist(option_values, epsilon=self.current_option_epsilon)
-        new_option_logp = option_dist.log_prob(options)
-        option_entropy = (option_dist.entropy() * boundary).sum() / n_bound
-        sel_w = loss_mask.unsqueeze(-1).to(dtype=option_dist.probs.dtype)
-        marginal = ((option_dist.probs * sel_w).sum(dim=(0, 1)) / sel_w.sum().clamp_min(1.0)).clamp_min(1e-8)
-        option_marginal_entropy = -(marginal * marginal.log()).sum()
-        option_balance_loss = (marginal * (marginal.log() + self._log_const(float(O), marginal))).sum()
-        effective_options = option_marginal_entropy.exp()
+        fused_opt = fused_option_terms(self.actor, option_values, options, loss_mask, boundary,
+                                       self.current_option_epsilon, d_bound)
+        if fused_opt is not None:
+            sum_logp, option_entropy, option_marginal_entropy, option_balance_loss, effective_options = fused_opt
+            behavior_option_logp_error = sum_logp * 0.0
+        else:
+            option_dist = self.actor.option_dist(option_values, epsilon=self.current_option_epsilon)
+            new_option_logp = option_dist.log_prob(options)
+            option_entropy = (option_dist.entropy() * boundary).sum() / n_bound
+            sel_w = loss_mask.unsqueeze(-1).to(dtype=option_dist.probs.dtype)
+            marginal = ((option_dist.probs * sel_w).sum(dim=(0, 1)) / sel_w.sum().clamp_min(1.0)).clamp_min(1e-8)
+            option_marginal_entropy = -(marginal * marginal.log()).sum()
+            option_balance_loss = (marginal * (marginal.log() + self._log_const(float(O), marginal))).sum()
+            effective_options = option_marginal_entropy.exp()
+            behavior_option_logp_error = new_option_logp.sum() * 0.0
         selector_loss = option_values.sum() * 0.0
         option_approx_kl = option_values.sum() * 0.0
-        behavior_option_logp_error = new_option_logp.sum() * 0.0
 
         # intra-option wheel policy: PPO against the frozen update-start actor (LOT:1095-1138)
         action_dist = self.actor.selected_action_dist(action_means, action_stds, options)
@@ -399,7 +532,6 @@ class LearnedOptionCriticTrainer(TrainerBase):
         (_s, next_option_values, next_term_logits, _m, _sd, _a, _n) = self.actor.step(
             next_obs.reshape(B * L, self.obs_dim), (next_h, next_c))
         next_beta_logits = self.actor.selected_termination_logits(next_term_logits, options.reshape(-1)).view(B, L)
-        next_beta = torch.sigmoid(next_beta_logits)
 
         flat_returns = batch["returns"].reshape(-1)
         flat_mask = loss_mask.reshape(-1)
@@ -431,19 +563,32 @@ class LearnedOptionCriticTrainer(TrainerBase):
                                                         epsilon=self.current_option_epsilon)
             termination_advantage = (next_q - reselection).view(B, L)
 
-        termination_loss = termination_objective(next_beta, termination_advantage, cfg.termination_penalty,
-                                                 term_mask, denom=n_term)
-        prior = F.binary_cross_entropy_with_logits(
-            next_beta_logits, torch.full_like(next_beta_logits, cfg.termination_prior_probability), reduction="none")
-        termination_prior_loss = (prior * term_mask).sum() / n_term
-        termination_entropy = (Bernoulli(validate_args=False, logits=next_beta_logits).entropy() * term_mask).sum() / n_term
-        mean_beta = (next_beta * term_mask).sum() / n_term
-        mean_termination_advantage = (termination_advantage * term_mask).sum() / n_term
-        mean_termination_signal = ((termination_advantage + cfg.termination_penalty) * term_mask).sum() / n_term
-        low_sat = ((next_beta < 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
-        high_sat = ((next_beta > 1.0 - 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
-        diversity, temporal, mean_attention = self._attention_losses(
-            attentions, loss_mask, dones, d_mask, d_pairs if d_pairs is not None else None)
+        fused_term = fused_termination_terms(next_beta_logits, termination_advantage, cfg.termination_penalty,
+                                             cfg.termination_prior_probability, term_mask, d_term)
+        if fused_term is not None:
+            (termination_loss, termination_prior_loss, termination_entropy, mean_beta, mean_termination_advantage,
+             mean_termination_signal, low_sat, high_sat) = fused_term
+        else:
+            next_beta = torch.sigmoid(next_beta_logits)
+            termination_loss = termination_objective(next_beta, termination_advantage, cfg.termination_penalty,
+                                                     term_mask, denom=n_term)
+            prior = F.binary_cross_entropy_with_logits(
+                next_beta_logits, torch.full_like(next_beta_logits, cfg.termination_prior_probability),
+                reduction="none")
+            termination_prior_loss = (prior * term_mask).sum() / n_term
+            termination_entropy = (Bernoulli(validate_args=False, logits=next_beta_logits).entropy()
+                                   * term_mask).sum() / n_term
+            mean_beta = (next_beta * term_mask).sum() / n_term
+            mean_termination_advantage = (termination_advantage * term_mask).sum() / n_term
+            mean_termination_signal = ((termination_advantage + cfg.termination_penalty) * term_mask).sum() / n_term
+            low_sat = ((next_beta < 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
+            high_sat = ((next_beta > 1.0 - 1e-3).to(next_beta.dtype) * term_mask).sum() / n_term
+        fused_att = fused_attention_terms(attentions, loss_mask, dones, d_mask, d_pairs)
+        if fused_att is not None:
+            diversity, temporal, mean_attention = fused_att
+        else:
+            diversity, temporal, mean_attention = self._attention_losses(
+                attentions, loss_mask, dones, d_mask, d_pairs if d_pairs is not None else None)
         return {
             "intra_option_loss": intra_option_loss, "selector_loss": selector_loss,
             "local_option_value_loss": local_option_value_loss, "local_option_value_mean": local_option_value_mean,

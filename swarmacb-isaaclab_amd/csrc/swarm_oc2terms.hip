@@ -1,0 +1,360 @@
+// swarm_oc2terms.hip — the learned-option (OC2) update's termination, option-selection and
+// attention terms (include/swarmtrain.h: swarm_oc2_termination_terms*, swarm_oc2_option_terms,
+// swarm_oc2_attention_terms*).
+//
+// Reference: LearnedOptionCriticTrainer._compute_sequence_losses (agents/
+// learned_option_critic_trainer.py:1050-1093 option selection, 1140-1169 + 1282-1317 termination,
+// 956-997 attention). Under autograd each group is dozens of small torch kernels per minibatch
+// (a sigmoid, three binary cross-entropies, masked sums and means, boolean masks, a matmul and an
+// index_select, abs / diff / mean, their backwards) — at the launch floor for a 2,048-row
+// minibatch. Here each group is ONE kernel forward (one workgroup reduces every term of the
+// minibatch and writes device scalars) and, where the actor objective differentiates it, ONE
+// elementwise kernel backward that reads the incoming gradients from device memory (graph
+// capturable, no host sync).
+//
+// Termination (rows m of the B x L minibatch; z = the selected termination logit at s',
+// a = the (no-grad) termination advantage, w = the term mask (1 - done) * loss_mask, n = the
+// denominator: `denom` if given, else max(sum w, 1)):
+//   beta = sigmoid(z);  out[0] termination loss  = sum beta (a + penalty) w / n   (LON:29-46)
+//   out[1] prior loss   = sum BCEwithlogits(z, p) w / n                          (LOT:1318-1322)
+//   out[2] entropy      = sum H(z) w / n, H = BCEwithlogits(z, sigmoid(z))        (Bernoulli.entropy)
+//   out[3..7] mean beta, mean a, mean (a + penalty), share(beta < 1e-3), share(beta > 1 - 1e-3)
+//   backward: dz = w / n * (g0 beta (1 - beta) (a + penalty) + g1 (beta - p) - g2 beta (1 - beta) z)
+// Option selection (AOC epsilon-greedy manager over Q_Omega, LON:562-589; no gradient: the
+// probabilities are built from an argmax): per row probs = low + greedy_add onehot(argmax q)
+// (low = fp32(eps / O), greedy_add = fp32(1 - eps): torch's full_like + scatter_add_), then
+// normalised as Categorical(probs=...) does, with logits log(clamp(p, eps32, 1 - eps32)):
+//   out[0] sum over ALL rows of log_prob(option) (the reference multiplies it by 0),
+//   out[1] option entropy = sum H(probs) boundary / n_b, H = -sum p logits,
+//   marginal_o = max(sum probs_o mask / max(sum mask, 1), 1e-8):
+//   out[2] marginal entropy -sum m log m, out[3] balance sum m (log m + log O), out[4] exp(out[2])
+// Attention (B sequences x L steps x O options x D features, a = attention weights):
+//   n_o = a_o / max(|a_o|, 1e-8); diversity = sum_rows active sum_{o != p} n_o.n_p / (n_r O (O-1))
+//   temporal = sum_{t < L-1} pair_t mean_{o,d} |a_{t+1} - a_t| / n_pairs,
+//              pair_t = mask_t & mask_{t+1} & done_t < 0.5
+//   mean attention = sum_rows active sum a / (n_r O D)
+//   backward: diversity through F.normalize (da = (g - n (n.g)) / |a|, or g / eps below eps),
+//   temporal through abs (sign, 0 at 0).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/swarmstep.h"
+#include "../../include/swarmtrain.h"
+
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr int kBwdThreads = 256;
+
+// block-wide sum of K per-thread partials; the result is valid in thread 0
+template <int K>
+__device__ __forceinline__ void block_sum(float (&v)[K]) {
+    __shared__ float red[K][kWaves];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[k][w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float s = 0.0f;
+            for (int i = 0; i < kWaves; ++i) s += red[k][i];
+            v[k] = s;
+        }
+    }
+}
+
+__device__ __forceinline__ float sigmoidf(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+// log(1 + exp(x)) without overflow
+__device__ __forceinline__ float softplusf(float x) { return fmaxf(x, 0.0f) + log1pf(expf(-fabsf(x))); }
+
+// torch.nn.functional.binary_cross_entropy_with_logits(z, y): (1 - y) z + log(1 + exp(-z))
+__device__ __forceinline__ float bce_logits(float z, float y) { return (1.0f - y) * z + softplusf(-z); }
+
+// ------------------------------------------------------------------- termination
+__global__ __launch_bounds__(kThreads) void term_fwd_kernel(int64_t M, const float* __restrict__ z,
+                                                            const float* __restrict__ adv,
+                                                            const float* __restrict__ w, const float* denom,
+                                                            float penalty, float prior_p, float* __restrict__ out,
+                                                            float* __restrict__ used_denom) {
+    float v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t m = threadIdx.x; m < M; m += kThreads) {
+        const float x = z[m], a = adv[m], wm = w[m];
+        const float b = sigmoidf(x);
+        v[0] += b * (a + penalty) * wm;
+        v[1] += bce_logits(x, prior_p) * wm;
+        v[2] += bce_logits(x, b) * wm;
+        v[3] += b * wm;
+        v[4] += a * wm;
+        v[5] += (a + penalty) * wm;
+        v[6] += (b < 1e-3f ? 1.0f : 0.0f) * wm;
+        v[7] += (b > 1.0f - 1e-3f ? 1.0f : 0.0f) * wm;
+        v[8] += wm;
+    }
+    block_sum<9>(v);
+    if (threadIdx.x == 0) {
+        const float n = denom ? *denom : fmaxf(v[8], 1.0f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = v[k] / n;
+        *used_denom = n;
+    }
+}
+
+__global__ __launch_bounds__(kBwdThreads) void term_bwd_kernel(int64_t M, const float* __restrict__ z,
+                                                               const float* __restrict__ adv,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ used_denom, float penalty,
+                                                               float prior_p, const float* __restrict__ g,
+                                                               float* __restrict__ dz) {
+    const int64_t m = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
+    if (m >= M) return;
+    const float x = z[m], b = sigmoidf(x);
+    const float s = w[m] / *used_denom;
+    const float db = b * (1.0f - b);
+    dz[m] = s * (g[0] * db * (adv[m] + penalty) + g[1] * (b - prior_p) - g[2] * db * x);
+}
+
+// ------------------------------------------------------------------- option selection
+constexpr int kMaxOptions = 16;
+
+__global__ __launch_bounds__(kThreads) void option_fwd_kernel(int64_t M, int O, const float* __restrict__ q,
+                                                              const int64_t* __restrict__ options,
+                                                              const uint8_t* __restrict__ mask,
+                                                              const uint8_t* __restrict__ boundary,
+                                                              const float* denom_b, float low, float greedy_add,
+                                                              float log_o, float* __restrict__ out) {
+    // partials: sum log p[option], sum H boundary, sum boundary, sum mask, marginal numerators
+    float v[4 + kMaxOptions];
+#pragma unroll
+    for (int k = 0; k < 4 + kMaxOptions; ++k) v[k] = 0.0f;
+    constexpr float kEps32 = 1.1920928955078125e-07f;   // torch.finfo(float32).eps (clamp_probs)
+    const float hi0 = low + greedy_add;
+    float tot = 0.0f;                                    // probs.sum(-1): (O - 1) x low + hi0
+    for (int o = 0; o < O - 1; ++o) tot += low;
+    tot += hi0;
+    const float lo = low / tot, hi = hi0 / tot;
+    const float llo = logf(fminf(fmaxf(lo, kEps32), 1.0f - kEps32)), lhi = logf(fminf(fmaxf(hi, kEps32), 1.0f - kEps32));
+    for (int64_t m = threadIdx.x; m < M; m += kThreads) {
+        const float* r = q + m * O;
+        int best = 0;
+        float bq = r[0];
+        for (int o = 1; o < O; ++o)
+            if (r[o] > bq) {   // torch.argmax: the first maximal entry
+                bq = r[o];
+                best = o;
+            }
+        const int64_t opt = options[m];
+        v[0] += opt == best ? lhi : llo;
+        // entropy of the row: (O - 1) cells of lo, one of hi
+        float h = 0.0f;
+        for (int o = 0; o < O; ++o) h -= o == best ? hi * lhi : lo * llo;
+        const float bm = boundary[m] ? 1.0f : 0.0f, mk = mask[m] ? 1.0f : 0.0f;
+        v[1] += h * bm;
+        v[2] += bm;
+        v[3] += mk;
+#pragma unroll
+        for (int o = 0; o < kMaxOptions; ++o)
+            if (o < O) v[4 + o] += (o == best ? hi : lo) * mk;
+    }
+    block_sum<4 + kMaxOptions>(v);
+    if (threadIdx.x == 0) {
+        const float nb = denom_b ? *denom_b : fmaxf(v[2], 1.0f);
+        const float nm = fmaxf(v[3], 1.0f);
+        float ent = 0.0f, bal = 0.0f;
+        for (int o = 0; o < O; ++o) {
+            const float mo = fmaxf(v[4 + o] / nm, 1e-8f);
+            const float lm = logf(mo);
+            ent -= mo * lm;
+            bal += mo * (lm + log_o);
+        }
+        out[0] = v[0];
+        out[1] = v[1] / nb;
+        out[2] = ent;
+        out[3] = bal;
+        out[4] = expf(ent);
+    }
+}
+
+// ------------------------------------------------------------------- attention
+constexpr int kMaxAttnO = 8;
+constexpr int kMaxAttnD = 64;
+
+__device__ __forceinline__ float row_norm(const float* a, int D) {
+    float s = 0.0f;
+    for (int d = 0; d < D; ++d) s += a[d] * a[d];
+    return fmaxf(sqrtf(s), 1e-8f);
+}
+
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(int B, int L, int O, int D, const float* __restrict__ att,
+                                                            const uint8_t* __restrict__ mask,
+                                                            const float* __restrict__ dones, const float* d_rows,
+                                                            const float* d_pairs, float* __restrict__ out,
+                                                            float* __restrict__ used) {
+    float v[5] = {0, 0, 0, 0, 0};   // diversity sum, temporal sum, attention sum, rows, pairs
+    const int64_t rows = (int64_t)B * L;
+    const int OD = O * D;
+    for (int64_t r = threadIdx.x; r < rows; r += kThreads) {
+        const float* a = att + r * OD;
+        const float act = mask[r] ? 1.0f : 0.0f;
+        float inv[kMaxAttnO];
+        for (int o = 0; o < O; ++o) inv[o] = 1.0f / row_norm(a + o * D, D);
+        float div = 0.0f, tot = 0.0f;
+        for (int o = 0; o < O; ++o) {
+            for (int p = 0; p < O; ++p) {
+                if (p == o) continue;
+                float dot = 0.0f;
+                for (int d = 0; d < D; ++d) dot += (a[o * D + d] * inv[o]) * (a[p * D + d] * inv[p]);
+                div += dot;
+            }
+            for (int d = 0; d < D; ++d) tot += a[o * D + d];
+        }
+        v[0] += div * act;
+        v[2] += tot * act;
+        v[3] += act;
+        const int t = (int)(r % L);
+        if (t < L - 1) {
+            const float pr = (mask[r] && mask[r + 1] && dones[r] < 0.5f) ? 1.0f : 0.0f;
+            float ad = 0.0f;
+            for (int k = 0; k < OD; ++k) ad += fabsf(a[OD + k] - a[k]);
+            v[1] += (ad / (float)OD) * pr;
+            v[4] += pr;
+        }
+    }
+    block_sum<5>(v);
+    if (threadIdx.x == 0) {
+        const float nr = d_rows ? *d_rows : fmaxf(v[3], 1.0f);
+        const float np = d_pairs ? *d_pairs : fmaxf(v[4], 1.0f);
+        out[0] = v[0] / (nr * (float)(O * (O - 1)));
+        out[1] = v[1] / np;
+        out[2] = v[2] / (nr * (float)OD);
+        used[0] = nr;
+        used[1] = np;
+    }
+}
+
+// one thread per (row, option): the diversity gradient of a_o and the temporal gradient of a_o
+// from the pairs (t-1, t) and (t, t+1)
+__global__ __launch_bounds__(kBwdThreads) void attn_bwd_kernel(int B, int L, int O, int D,
+                                                               const float* __restrict__ att,
+                                                               const uint8_t* __restrict__ mask,
+                                                               const float* __restrict__ dones,
+                                                               const float* __restrict__ used,
+                                                               const float* __restrict__ g,
+                                                               float* __restrict__ datt) {
+    const int64_t i = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
+    const int64_t rows = (int64_t)B * L;
+    if (i >= rows * O) return;
+    const int64_t r = i / O;
+    const int o = (int)(i - r * O);
+    const int t = (int)(r % L);
+    const int OD = O * D;
+    const float* a = att + r * OD;
+    float* da = datt + r * OD + o * D;
+    const float gd = g[0] * (mask[r] ? 1.0f : 0.0f) / (used[0] * (float)(O * (O - 1)));
+    const float gt = g[1] / (used[1] * (float)OD);
+    const float w_next = (t < L - 1 && mask[r] && mask[r + 1] && dones[r] < 0.5f) ? gt : 0.0f;
+    const float w_prev = (t > 0 && mask[r - 1] && mask[r] && dones[r - 1] < 0.5f) ? gt : 0.0f;
+    // diversity: dS/dn_o = 2 sum_{p != o} n_p, then F.normalize's backward
+    const float nrm_o = row_norm(a + o * D, D);
+    const float inv_o = 1.0f / nrm_o;
+    float gn[kMaxAttnD];
+    for (int d = 0; d < D; ++d) gn[d] = 0.0f;
+    for (int p = 0; p < O; ++p) {
+        if (p == o) continue;
+        const float inv_p = 1.0f / row_norm(a + p * D, D);
+        for (int d = 0; d < D; ++d) gn[d] += a[p * D + d] * inv_p;
+    }
+    float ndotg = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        gn[d] *= 2.0f * gd;
+        ndotg += (a[o * D + d] * inv_o) * gn[d];
+    }
+    const bool clamped = nrm_o <= 1e-8f;   // x / max(|x|, eps): below eps the norm carries no gradient
+    for (int d = 0; d < D; ++d) {
+        const float x = a[o * D + d];
+        float v = clamped ? gn[d] * inv_o : (gn[d] - (x * inv_o) * ndotg) * inv_o;
+        if (w_next != 0.0f) {
+            const float df = a[OD + o * D + d] - x;
+            v -= w_next * (df > 0.0f ? 1.0f : (df < 0.0f ? -1.0f : 0.0f));
+        }
+        if (w_prev != 0.0f) {
+            const float df = x - a[-OD + o * D + d];
+            v += w_prev * (df > 0.0f ? 1.0f : (df < 0.0f ? -1.0f : 0.0f));
+        }
+        da[d] = v;
+    }
+}
+
+int32_t status() { return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t swarm_oc2_termination_terms(int64_t M, const float* logits, const float* advantages, const float* term_mask,
+                                    const float* denom, float penalty, float prior_probability, float* out,
+                                    float* used_denom, void* stream) {
+    if (M < 1 || !logits || !advantages || !term_mask || !out || !used_denom) return SWARM_ERR_ARG;
+    term_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(M, logits, advantages, term_mask, denom,
+                                                                          penalty, prior_probability, out,
+                                                                          used_denom);
+    return status();
+}
+
+int32_t swarm_oc2_termination_terms_backward(int64_t M, const float* logits, const float* advantages,
+                                             const float* term_mask, const float* used_denom, float penalty,
+                                             float prior_probability, const float* grads, float* d_logits,
+                                             void* stream) {
+    if (M < 1 || !logits || !advantages || !term_mask || !used_denom || !grads || !d_logits) return SWARM_ERR_ARG;
+    const int64_t blocks = (M + kBwdThreads - 1) / kBwdThreads;
+    if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
+    term_bwd_kernel<<<(unsigned)blocks, kBwdThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        M, logits, advantages, term_mask, used_denom, penalty, prior_probability, grads, d_logits);
+    return status();
+}
+
+int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values, const int64_t* options,
+                               const uint8_t* loss_mask, const uint8_t* boundary, const float* boundary_denom,
+                               float low, float greedy_add, float log_num_options, float* out, void* stream) {
+    if (M < 1 || O < 1 || O > kMaxOptions || !option_values || !options || !loss_mask || !boundary || !out)
+        return SWARM_ERR_ARG;
+    option_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        M, O, option_values, options, loss_mask, boundary, boundary_denom, low, greedy_add, log_num_options, out);
+    return status();
+}
+
+int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
+                                  const uint8_t* loss_mask, const float* dones, const float* row_denom,
+                                  const float* pair_denom, float* out, float* used_denoms, void* stream) {
+    if (B < 1 || L < 1 || O < 2 || O > kMaxAttnO || D < 1 || D > kMaxAttnD || !attentions || !loss_mask || !dones ||
+        !out || !used_denoms || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
+        return SWARM_ERR_ARG;
+    attn_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask, dones,
+                                                                          row_denom, pair_denom, out, used_denoms);
+    return status();
+}
+
+int32_t swarm_oc2_attention_terms_backward(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
+                                           const uint8_t* loss_mask, const float* dones, const float* used_denoms,
+                                           const float* grads, float* d_attentions, void* stream) {
+    if (B < 1 || L < 1 || O < 2 || O > kMaxAttnO || D < 1 || D > kMaxAttnD || !attentions || !loss_mask || !dones ||
+        !used_denoms || !grads || !d_attentions || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
+        return SWARM_ERR_ARG;
+    const int64_t n = (int64_t)B * L * O;
+    attn_bwd_kernel<<<(unsigned)((n + kBwdThreads - 1) / kBwdThreads), kBwdThreads, 0,
+                      static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask, dones, used_denoms,
+                                                          grads, d_attentions);
+    return status();
+}
+
+}  // extern "C"

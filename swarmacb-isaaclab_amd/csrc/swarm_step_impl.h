@@ -109,6 +109,14 @@
 #define SWARM_LAST_CACHE 0
 #endif
 
+// 1: the proximity rays of a near wall segment are pre-tested wave-uniformly with a
+// superset of the hit test (the ray points at the segment's line, t in [0, range] from
+// the signs and magnitudes of the two cross products, no reciprocal): a ray no active
+// lane can hit is skipped (it would leave every reading unchanged). Bitwise-neutral.
+#ifndef SWARM_RAY_PREFILTER
+#define SWARM_RAY_PREFILTER 0
+#endif
+
 // 1: the contact solver's pair term from one hardware reciprocal square root
 // (dist = s * rsq(s), the normal d * rsq(s)) instead of a correctly rounded sqrt
 // and a reciprocal of dist + 1e-8: the same formula within ~2 ulp of dist, i.e.
@@ -862,9 +870,20 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
 #endif
         const float qx = ax - x, qy = ay - y;
+#if SWARM_RAY_PREFILTER
+        const float qs = qx * sy - qy * sx;
+#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float den = rdx[k] * sy - rdy[k] * sx;
+#if SWARM_RAY_PREFILTER
+            // t = qs / den (via v_rcp of den + 1e-12, within 1e-4 relative of 1 / den for
+            // |den| > 1e-8): t >= 0 needs qs, den of one sign, t <= range needs |qs| <= range |den|
+            // (a 1e-3 margin covers the reciprocal's rounding)
+            if (!__any((fabsf(den) > 1e-8f) & (qs * den >= 0.0f) &
+                       (fabsf(qs) <= g.prox_range * 1.001f * fabsf(den))))
+                continue;
+#endif
             const bool valid = fabsf(den) > 1e-8f;
             const float dd = den + 1e-12f;
             const float inv = frcp(dd);

@@ -1,0 +1,116 @@
+"""The OC2 update's termination, option-selection and attention terms on one kernel each way
+(csrc/swarm_oc2terms.hip) against the torch formulation of the same terms
+(LearnedOptionCriticTrainer._compute_sequence_losses, LOT:956-997, 1050-1093, 1282-1322):
+forward values and the logits' / attentions' gradients, with local and given denominators,
+degenerate rows (zero-norm attention vectors, unchanged consecutive attentions, saturated
+logits, epsilon 0 and 1). The trainers' teacher-forced OC2 tests run the fused path too."""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch.distributions import Bernoulli, Categorical
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol, what):
+    a, b = a.detach().double(), b.detach().double()
+    scale = max(1.0, float(b.abs().max()))
+    err = float((a - b).abs().max())
+    assert err <= tol * scale, f"{what}: max err {err:.3g} (scale {scale:.3g})"
+
+
+@pytest.mark.parametrize("with_denom", [False, True])
+def test_termination_terms(with_denom, gpu_device):
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+
+    g = torch.Generator(device=gpu_device).manual_seed(3 + with_denom)
+    B, L = 16, 128
+    z0 = torch.randn(B, L, device=gpu_device, generator=g) * 3
+    z0[0, :4] = torch.tensor([40.0, -40.0, 0.0, 1e-3])           # saturated and neutral logits
+    adv = torch.randn(B, L, device=gpu_device, generator=g)
+    loss_mask = torch.rand(B, L, device=gpu_device, generator=g) > 0.2
+    dones = (torch.rand(B, L, device=gpu_device, generator=g) > 0.9).float()
+    term_mask = (1.0 - dones) * loss_mask
+    denom = torch.tensor(1500.0, device=gpu_device) if with_denom else None
+    pen, prior_p = 0.01, 0.27
+    coef = torch.tensor([0.7, -0.3, 1.3], device=gpu_device)
+    outs = []
+    for fused in (True, False):
+        z = z0.clone().requires_grad_(True)
+        n = denom if denom is not None else term_mask.sum().clamp_min(1.0)
+        if fused:
+            t = LT.fused_termination_terms(z, adv, pen, prior_p, term_mask, denom)
+            assert t is not None
+        else:
+            beta = torch.sigmoid(z)
+            t = ((beta * (adv + pen) * term_mask).sum() / n,
+                 (F.binary_cross_entropy_with_logits(z, torch.full_like(z, prior_p), reduction="none")
+                  * term_mask).sum() / n,
+                 (Bernoulli(validate_args=False, logits=z).entropy() * term_mask).sum() / n,
+                 (beta * term_mask).sum() / n, (adv * term_mask).sum() / n, ((adv + pen) * term_mask).sum() / n,
+                 ((beta < 1e-3).float() * term_mask).sum() / n, ((beta > 1 - 1e-3).float() * term_mask).sum() / n)
+        (coef[0] * t[0] + coef[1] * t[1] + coef[2] * t[2]).backward()
+        outs.append((torch.stack([x.detach() for x in t]), z.grad.clone()))
+    _close(outs[0][0], outs[1][0], 2e-6, "termination terms")
+    _close(outs[0][1], outs[1][1], 2e-6, "d logits")
+
+
+@pytest.mark.parametrize("eps", [0.0, 0.1, 1.0])
+def test_option_terms(eps, gpu_device):
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+
+    g = torch.Generator(device=gpu_device).manual_seed(int(eps * 10))
+    B, L, O = 16, 128, 6
+    q = torch.randn(B, L, O, device=gpu_device, generator=g)
+    q[0, 0] = 1.0                                                  # a tie: argmax takes the first
+    options = torch.randint(0, O, (B, L), device=gpu_device, generator=g)
+    loss_mask = torch.rand(B, L, device=gpu_device, generator=g) > 0.3
+    boundary = (torch.rand(B, L, device=gpu_device, generator=g) > 0.6) & loss_mask
+
+    class Actor:
+        epsilon_greedy_selector = True
+
+    got = LT.fused_option_terms(Actor(), q, options, loss_mask, boundary, eps, None)
+    probs = torch.full_like(q, eps / O)
+    greedy = q.argmax(dim=-1, keepdim=True)
+    probs.scatter_add_(-1, greedy, torch.full_like(greedy, 1.0 - eps, dtype=probs.dtype))
+    dist = Categorical(validate_args=False, probs=probs)
+    n_b = boundary.sum().clamp_min(1)
+    sel_w = loss_mask.unsqueeze(-1).float()
+    marginal = ((dist.probs * sel_w).sum(dim=(0, 1)) / sel_w.sum().clamp_min(1.0)).clamp_min(1e-8)
+    ent = -(marginal * marginal.log()).sum()
+    ref = torch.stack([dist.log_prob(options).sum(), (dist.entropy() * boundary).sum() / n_b, ent,
+                       (marginal * (marginal.log() + torch.log(torch.tensor(float(O), device=gpu_device)))).sum(),
+                       ent.exp()])
+    _close(torch.stack(got), ref, 2e-6, "option terms")
+
+
+@pytest.mark.parametrize("with_denom", [False, True])
+def test_attention_terms(with_denom, gpu_device):
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+    from SwarmACB_isaac.agents.learned_option_critic_trainer import LearnedOptionCriticTrainer
+
+    g = torch.Generator(device=gpu_device).manual_seed(7 + with_denom)
+    B, L, O, D = 16, 128, 6, 24
+    a0 = torch.sigmoid(torch.randn(B, L, O, D, device=gpu_device, generator=g) * 2)
+    a0[0, 3, 2] = 0.0                                                # a zero-norm option vector
+    a0[1, 5] = a0[1, 4]                                              # unchanged step (abs' kink)
+    loss_mask = torch.rand(B, L, device=gpu_device, generator=g) > 0.2
+    dones = (torch.rand(B, L, device=gpu_device, generator=g) > 0.9).float()
+    d_rows = torch.tensor(1700.0, device=gpu_device) if with_denom else None
+    d_pairs = torch.tensor(1400.0, device=gpu_device) if with_denom else None
+    outs = []
+    for fused in (True, False):
+        a = a0.clone().requires_grad_(True)
+        if fused:
+            t = LT.fused_attention_terms(a, loss_mask, dones, d_rows, d_pairs)
+            assert t is not None
+        else:
+            t = LearnedOptionCriticTrainer._attention_losses(a, loss_mask, dones, d_rows, d_pairs)
+        (0.9 * t[0] - 1.7 * t[1]).backward()
+        outs.append((torch.stack([x.detach() for x in t]), a.grad.clone()))
+    _close(outs[0][0], outs[1][0], 2e-6, "attention terms")
+    _close(outs[0][1], outs[1][1], 2e-6, "d attentions")
