@@ -189,7 +189,10 @@ int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logi
  *     marginal entropy, balance, effective options, over M rows of O <= 16 option values; low =
  *     fp32(eps / O), greedy_add = fp32(1 - eps), log_num_options = fp32 log(O);
  *   attention: out[3] = diversity, temporal, mean attention over (B, L, O <= 8, D <= 64) weights;
- *     used_denoms[2] = the row and pair denominators; grads[2] = d/d out[0..1]. */
+ *     used_denoms[2] = the row and pair denominators; grads[2] = d/d out[0..1];
+ *   action terms: log_probs / ref_log_probs (M, A) of the (squashed) Normal wheel policy of the
+ *     current and the frozen actor, out[3] = approx KL, behaviour error, action entropy;
+ *     grad_log_probs (M, A) and grad_out[3] (either may be NULL) -> d_means, d_stds (M, A). */
 int32_t swarm_oc2_termination_terms(int64_t M, const float* logits, const float* advantages, const float* term_mask,
                                     const float* denom, float penalty, float prior_probability, float* out,
                                     float* used_denom, void* stream);
@@ -200,6 +203,14 @@ int32_t swarm_oc2_termination_terms_backward(int64_t M, const float* logits, con
 int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values, const int64_t* options,
                                const uint8_t* loss_mask, const uint8_t* boundary, const float* boundary_denom,
                                float low, float greedy_add, float log_num_options, float* out, void* stream);
+int32_t swarm_oc2_action_terms(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
+                               const float* ref_means, const float* ref_stds, const float* actions,
+                               const float* old_log_probs, const uint8_t* loss_mask, const float* row_denom,
+                               float* log_probs, float* ref_log_probs, float* out, float* used_denom, void* stream);
+int32_t swarm_oc2_action_terms_backward(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
+                                        const float* actions, const uint8_t* loss_mask, const float* used_denom,
+                                        const float* grad_log_probs, const float* grad_out, float* d_means,
+                                        float* d_stds, void* stream);
 int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
                                   const uint8_t* loss_mask, const float* dones, const float* row_denom,
                                   const float* pair_denom, float* out, float* used_denoms, void* stream);

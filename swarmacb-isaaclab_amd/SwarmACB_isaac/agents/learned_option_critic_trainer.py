@@ -162,6 +162,65 @@ class _AttentionTerms(torch.autograd.Function):
         return da, None, None, None, None
 
 
+class _ActionTerms(torch.autograd.Function):
+    """The intra-option wheel-policy terms of the OC2 losses on swarm_oc2_action_terms / _backward:
+    the selected option's means / stds (M, A) of the current actor (differentiated) and of the
+    frozen reference actor -> (new log-probs (M, A), reference log-probs (M, A), out (3,) = approx KL,
+    behaviour error, action entropy)."""
+
+    @staticmethod
+    def forward(ctx, means, stds, ref_means, ref_stds, actions, old_lp, mask_u8, row_denom, squashed: bool):
+        mu, sg = means.contiguous(), stds.contiguous()
+        M, A = mu.shape
+        lp = torch.empty_like(mu)
+        lp_r = torch.empty_like(mu)
+        out = torch.empty(3, dtype=mu.dtype, device=mu.device)
+        used = torch.empty((), dtype=mu.dtype, device=mu.device)
+        _native.check(_native.load().swarm_oc2_action_terms(
+            M, A, int(squashed), _vp(mu), _vp(sg), _vp(ref_means), _vp(ref_stds), _vp(actions), _vp(old_lp),
+            _vp(mask_u8), _vp(row_denom), _vp(lp), _vp(lp_r), _vp(out), _vp(used), _stream(mu)),
+            "swarm_oc2_action_terms")
+        ctx.save_for_backward(mu, sg, actions, mask_u8, used)
+        ctx.squashed = bool(squashed)
+        ctx.mark_non_differentiable(lp_r)
+        return lp, lp_r, out
+
+    @staticmethod
+    def backward(ctx, d_lp, _d_lp_r, d_out):
+        mu, sg, actions, mask_u8, used = ctx.saved_tensors
+        M, A = mu.shape
+        d_mu, d_sg = torch.empty_like(mu), torch.empty_like(sg)
+        g_lp = d_lp.contiguous() if d_lp is not None else None
+        g_out = d_out.contiguous() if d_out is not None else None
+        _native.check(_native.load().swarm_oc2_action_terms_backward(
+            M, A, int(ctx.squashed), _vp(mu), _vp(sg), _vp(actions), _vp(mask_u8), _vp(used), _vp(g_lp), _vp(g_out),
+            _vp(d_mu), _vp(d_sg), _stream(mu)), "swarm_oc2_action_terms_backward")
+        return d_mu, d_sg, None, None, None, None, None, None, None
+
+
+def fused_action_terms(actor, action_means, action_stds, ref_means, ref_stds, options, actions, old_log_probs,
+                       loss_mask, row_denom):
+    """(new log-probs (B, L, A), reference log-probs, approx KL, behaviour error, action entropy) of
+    LOT:1095-1138 (the option's wheel distribution gathered by torch, the rest one kernel each way),
+    or None when the inputs do not fit it."""
+    d = _scalar_denom(row_denom)
+    if not (FUSED_OC2_TERMS and action_means.is_cuda and action_means.dtype == torch.float32 and d is not False
+            and actions.dtype == torch.float32 and old_log_probs.dtype == torch.float32 and actions.numel() > 0):
+        return None
+    means = actor._gather_options(action_means, options)
+    stds = actor._gather_options(action_stds, options)
+    with torch.no_grad():
+        r_means = actor._gather_options(ref_means, options).reshape(-1, means.shape[-1]).contiguous()
+        r_stds = actor._gather_options(ref_stds, options).reshape(-1, means.shape[-1]).contiguous()
+    shape = means.shape
+    A = shape[-1]
+    m = loss_mask.reshape(-1).to(torch.bool).contiguous().view(torch.uint8)
+    lp, lp_r, out = _ActionTerms.apply(means.reshape(-1, A), stds.reshape(-1, A), r_means, r_stds,
+                                       actions.reshape(-1, A).contiguous(),
+                                       old_log_probs.reshape(-1, A).contiguous(), m, d, actor.squash_actions)
+    return lp.view(shape), lp_r.view(shape), out[0], out[1], out[2]
+
+
 def fused_termination_terms(next_beta_logits, termination_advantage, penalty, prior_p, term_mask, denom):
     """(termination loss, prior loss, entropy, mean beta, mean advantage, mean signal, low, high) of
     LOT:1282-1322 in one kernel each way, or None when the inputs do not fit it."""
@@ -511,20 +570,30 @@ class LearnedOptionCriticTrainer(TrainerBase):
         option_approx_kl = option_values.sum() * 0.0
 
         # intra-option wheel policy: PPO against the frozen update-start actor (LOT:1095-1138)
-        action_dist = self.actor.selected_action_dist(action_means, action_stds, options)
-        new_action_logp = action_dist.log_prob(actions)
-        with torch.no_grad():
-            ref_action_logp = reference_actor.selected_action_dist(ref_means, ref_stds, options).log_prob(actions)
-        log_ratio = (new_action_logp - ref_action_logp).clamp(-20.0, 20.0)
-        kl_w = loss_mask.unsqueeze(-1).expand_as(log_ratio).to(log_ratio.dtype)
-        n_kl = n_mask_f * A if d_mask is not None else kl_w.sum().clamp_min(1.0)
-        action_approx_kl = ((log_ratio.exp() - 1.0 - log_ratio) * kl_w).sum() / n_kl
-        behavior_action_logp_error = ((ref_action_logp - batch["old_action_log_probs"]).abs() * kl_w).sum() / n_kl
+        fused_act = None
+        if reference_actor.squash_actions == self.actor.squash_actions:
+            fused_act = fused_action_terms(self.actor, action_means, action_stds, ref_means, ref_stds, options,
+                                           actions, batch["old_action_log_probs"], loss_mask, d_mask)
+        if fused_act is not None:
+            new_action_logp, ref_action_logp, action_approx_kl, behavior_action_logp_error, action_entropy = \
+                fused_act
+        else:
+            action_dist = self.actor.selected_action_dist(action_means, action_stds, options)
+            new_action_logp = action_dist.log_prob(actions)
+            with torch.no_grad():
+                ref_action_logp = reference_actor.selected_action_dist(ref_means, ref_stds, options).log_prob(
+                    actions)
+            log_ratio = (new_action_logp - ref_action_logp).clamp(-20.0, 20.0)
+            kl_w = loss_mask.unsqueeze(-1).expand_as(log_ratio).to(log_ratio.dtype)
+            n_kl = n_mask_f * A if d_mask is not None else kl_w.sum().clamp_min(1.0)
+            action_approx_kl = ((log_ratio.exp() - 1.0 - log_ratio) * kl_w).sum() / n_kl
+            behavior_action_logp_error = ((ref_action_logp - batch["old_action_log_probs"]).abs()
+                                          * kl_w).sum() / n_kl
+            action_entropy = (action_dist.entropy().mean(dim=-1) * loss_mask).sum() / n_mask
         intra_option_loss = stable_trust_region_policy_loss(
             batch["action_advantages"].reshape(-1, 1).detach(), new_action_logp.reshape(-1, A),
             ref_action_logp.reshape(-1, A), current_eps, loss_mask.reshape(-1),
             denom=n_mask_f * A if d_mask is not None else None)
-        action_entropy = (action_dist.entropy().mean(dim=-1) * loss_mask).sum() / n_mask
 
         # termination logits at s' from the stored post-decision memory (LOT:1140-1169)
         next_h = batch["next_memory_h"].reshape(B * L, -1).unsqueeze(0).detach()

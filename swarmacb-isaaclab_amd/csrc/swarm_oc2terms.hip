@@ -35,6 +35,17 @@
 //   mean attention = sum_rows active sum a / (n_r O D)
 //   backward: diversity through F.normalize (da = (g - n (n.g)) / |a|, or g / eps below eps),
 //   temporal through abs (sign, 0 at 0).
+// Action terms (the intra-option wheel policy of LOT:1095-1138, M rows x A wheels; mu / sigma the
+// selected option's mean / std of the current actor, mu_r / sigma_r of the frozen update-start
+// actor; x the taken action): u = atanh(clamp(x, +-(1 - 1e-6))) as 0.5 (log1p(b) - log1p(-b))
+// when the actions are squashed (else u = x), log|det| = 2 (log 2 - u - softplus(-2u)) (0
+// unsquashed), logp = -(u - mu)^2 / (2 sigma^2) - log sigma - log sqrt(2 pi) - log|det|;
+//   outputs new logp (M, A), ref logp (M, A), and out[3] = approx KL sum w (e^r - 1 - r) / n_kl
+//   (r = clamp(logp - logp_ref, +-20)), behaviour error sum w |logp_ref - logp_old| / n_kl,
+//   action entropy sum_rows mask mean_a (0.5 + log sqrt(2 pi) + log sigma) / n_mask;
+//   n_kl = A x (given row denominator) or max(A x sum mask, 1), n_mask = given or max(sum mask, 1)
+//   backward: d mu = g_lp (u - mu) / sigma^2, d sigma = g_lp ((u - mu)^2 / sigma^3 - 1 / sigma)
+//             + g_ent mask / (n_mask A sigma)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -295,6 +306,86 @@ __global__ __launch_bounds__(kBwdThreads) void attn_bwd_kernel(int B, int L, int
     }
 }
 
+// ------------------------------------------------------------------- action terms
+constexpr float kLogSqrt2Pi = 0.91893853320467274178f;   // math.log(math.sqrt(2 * math.pi))
+constexpr float kLog2 = 0.69314718055994530942f;         // math.log(2.0)
+
+__device__ __forceinline__ float pre_tanh_of(float x, bool squash, float& logdet) {
+    if (!squash) {
+        logdet = 0.0f;
+        return x;
+    }
+    const float b = fminf(fmaxf(x, -1.0f + 1e-6f), 1.0f - 1e-6f);
+    const float u = 0.5f * (log1pf(b) - log1pf(-b));
+    logdet = 2.0f * (kLog2 - u - softplusf(-2.0f * u));
+    return u;
+}
+
+__device__ __forceinline__ float normal_logp(float u, float mu, float sigma) {
+    const float d = u - mu;
+    return -(d * d) / (2.0f * (sigma * sigma)) - logf(sigma) - kLogSqrt2Pi;
+}
+
+__global__ __launch_bounds__(kThreads) void action_fwd_kernel(int64_t M, int A, int squash,
+                                                              const float* __restrict__ mu,
+                                                              const float* __restrict__ sg,
+                                                              const float* __restrict__ mu_r,
+                                                              const float* __restrict__ sg_r,
+                                                              const float* __restrict__ x,
+                                                              const float* __restrict__ old_lp,
+                                                              const uint8_t* __restrict__ mask,
+                                                              const float* row_denom, float* __restrict__ lp,
+                                                              float* __restrict__ lp_r, float* __restrict__ out,
+                                                              float* __restrict__ used) {
+    float v[4] = {0, 0, 0, 0};   // kl sum, behaviour sum, entropy sum, mask count
+    const int64_t n = M * A;
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+        const int64_t m = i / A;
+        float ld;
+        const float u = pre_tanh_of(x[i], squash != 0, ld);
+        const float a = normal_logp(u, mu[i], sg[i]) - ld;
+        const float b = normal_logp(u, mu_r[i], sg_r[i]) - ld;
+        lp[i] = a;
+        lp_r[i] = b;
+        const float w = mask[m] ? 1.0f : 0.0f;
+        const float r = fminf(fmaxf(a - b, -20.0f), 20.0f);
+        v[0] += (expf(r) - 1.0f - r) * w;
+        v[1] += fabsf(b - old_lp[i]) * w;
+        v[2] += (0.5f + kLogSqrt2Pi + logf(sg[i])) * w;   // Normal.entropy, summed over the row's wheels
+        if (i - m * A == 0) v[3] += w;
+    }
+    block_sum<4>(v);
+    if (threadIdx.x == 0) {
+        const float nm = row_denom ? *row_denom : fmaxf(v[3], 1.0f);
+        const float nkl = row_denom ? *row_denom * (float)A : fmaxf(v[3] * (float)A, 1.0f);
+        out[0] = v[0] / nkl;
+        out[1] = v[1] / nkl;
+        out[2] = (v[2] / (float)A) / nm;
+        used[0] = nm;
+    }
+}
+
+__global__ __launch_bounds__(kBwdThreads) void action_bwd_kernel(int64_t M, int A, int squash,
+                                                                 const float* __restrict__ mu,
+                                                                 const float* __restrict__ sg,
+                                                                 const float* __restrict__ x,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 const float* __restrict__ used,
+                                                                 const float* __restrict__ g_lp,
+                                                                 const float* __restrict__ g_out,
+                                                                 float* __restrict__ d_mu, float* __restrict__ d_sg) {
+    const int64_t i = (int64_t)blockIdx.x * kBwdThreads + threadIdx.x;
+    if (i >= M * A) return;
+    const int64_t m = i / A;
+    float ld;
+    const float u = pre_tanh_of(x[i], squash != 0, ld);
+    const float s = sg[i], d = u - mu[i];
+    const float g = g_lp ? g_lp[i] : 0.0f;
+    const float ge = g_out ? g_out[2] * (mask[m] ? 1.0f : 0.0f) / (*used * (float)A) : 0.0f;
+    d_mu[i] = g * d / (s * s);
+    d_sg[i] = g * (d * d / (s * s * s) - 1.0f / s) + ge / s;
+}
+
 int32_t status() { return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP; }
 
 }  // namespace
@@ -354,6 +445,32 @@ int32_t swarm_oc2_attention_terms_backward(int32_t B, int32_t L, int32_t O, int3
     attn_bwd_kernel<<<(unsigned)((n + kBwdThreads - 1) / kBwdThreads), kBwdThreads, 0,
                       static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask, dones, used_denoms,
                                                           grads, d_attentions);
+    return status();
+}
+
+int32_t swarm_oc2_action_terms(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
+                               const float* ref_means, const float* ref_stds, const float* actions,
+                               const float* old_log_probs, const uint8_t* loss_mask, const float* row_denom,
+                               float* log_probs, float* ref_log_probs, float* out, float* used_denom, void* stream) {
+    if (M < 1 || A < 1 || !means || !stds || !ref_means || !ref_stds || !actions || !old_log_probs || !loss_mask ||
+        !log_probs || !ref_log_probs || !out || !used_denom)
+        return SWARM_ERR_ARG;
+    action_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        M, A, squashed, means, stds, ref_means, ref_stds, actions, old_log_probs, loss_mask, row_denom, log_probs,
+        ref_log_probs, out, used_denom);
+    return status();
+}
+
+int32_t swarm_oc2_action_terms_backward(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
+                                        const float* actions, const uint8_t* loss_mask, const float* used_denom,
+                                        const float* grad_log_probs, const float* grad_out, float* d_means,
+                                        float* d_stds, void* stream) {
+    if (M < 1 || A < 1 || !means || !stds || !actions || !loss_mask || !used_denom || !d_means || !d_stds)
+        return SWARM_ERR_ARG;
+    const int64_t blocks = (M * A + kBwdThreads - 1) / kBwdThreads;
+    if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
+    action_bwd_kernel<<<(unsigned)blocks, kBwdThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        M, A, squashed, means, stds, actions, loss_mask, used_denom, grad_log_probs, grad_out, d_means, d_stds);
     return status();
 }
 

@@ -114,3 +114,58 @@ def test_attention_terms(with_denom, gpu_device):
         outs.append((torch.stack([x.detach() for x in t]), a.grad.clone()))
     _close(outs[0][0], outs[1][0], 2e-6, "attention terms")
     _close(outs[0][1], outs[1][1], 2e-6, "d attentions")
+
+
+@pytest.mark.parametrize("squash,with_denom", [(False, False), (True, False), (True, True)])
+def test_action_terms(squash, with_denom, gpu_device):
+    """Intra-option wheel terms: the option's Normal / tanh-squashed Normal log-probs of the current
+    and the frozen actor, approx KL, behaviour error and entropy, and the gradients of
+    (PPO-style weights on the new log-probs + an entropy coefficient) w.r.t. means and stds."""
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+    from SwarmACB_isaac.agents.learned_option_critic_networks import LearnedOptionActor, SquashedNormal
+    from torch.distributions import Normal
+
+    g = torch.Generator(device=gpu_device).manual_seed(11 + squash + 2 * with_denom)
+    B, L, O, A = 16, 128, 6, 2
+    means0 = torch.randn(B, L, O, A, device=gpu_device, generator=g) * 0.5
+    stds0 = torch.rand(B, L, O, A, device=gpu_device, generator=g) * 0.5 + 0.1
+    r_means = means0 + 0.05 * torch.randn(B, L, O, A, device=gpu_device, generator=g)
+    r_stds = stds0 * (1 + 0.05 * torch.rand(B, L, O, A, device=gpu_device, generator=g))
+    options = torch.randint(0, O, (B, L), device=gpu_device, generator=g)
+    actions = torch.tanh(torch.randn(B, L, A, device=gpu_device, generator=g)) if squash else \
+        torch.randn(B, L, A, device=gpu_device, generator=g)
+    if squash:
+        actions[0, 0] = torch.tensor([1.0, -1.0])                       # clamped to +-(1 - 1e-6)
+    old_lp = torch.randn(B, L, A, device=gpu_device, generator=g)
+    loss_mask = torch.rand(B, L, device=gpu_device, generator=g) > 0.25
+    d_mask = torch.tensor(1700.0, device=gpu_device) if with_denom else None
+    w_lp = torch.randn(B, L, A, device=gpu_device, generator=g)
+    actor = LearnedOptionActor(24, A, O, hidden=16, option_hidden=16, option_memory_size=8, memory_size=16,
+                               squash_actions=squash).to(gpu_device)
+    outs = []
+    for fused in (True, False):
+        mu = means0.clone().requires_grad_(True)
+        sd = stds0.clone().requires_grad_(True)
+        if fused:
+            lp, lp_r, kl, beh, ent = LT.fused_action_terms(actor, mu, sd, r_means, r_stds, options, actions, old_lp,
+                                                           loss_mask, d_mask)
+        else:
+            dist_cls = SquashedNormal if squash else Normal
+            m_ = actor._gather_options(mu, options)
+            s_ = actor._gather_options(sd, options)
+            dist = dist_cls(m_, s_, validate_args=False)
+            lp = dist.log_prob(actions)
+            lp_r = dist_cls(actor._gather_options(r_means, options), actor._gather_options(r_stds, options),
+                            validate_args=False).log_prob(actions)
+            lr = (lp - lp_r).clamp(-20.0, 20.0)
+            kw = loss_mask.unsqueeze(-1).expand_as(lr).float()
+            n_kl = d_mask * A if d_mask is not None else kw.sum().clamp_min(1.0)
+            n_m = d_mask if d_mask is not None else loss_mask.sum().clamp_min(1)
+            kl = ((lr.exp() - 1.0 - lr) * kw).sum() / n_kl
+            beh = ((lp_r - old_lp).abs() * kw).sum() / n_kl
+            ent = (dist.entropy().mean(dim=-1) * loss_mask).sum() / n_m
+        ((lp * w_lp).sum() - 0.37 * ent).backward()
+        outs.append((lp.detach(), lp_r.detach(), torch.stack([kl.detach(), beh.detach(), ent.detach()]),
+                     mu.grad.clone(), sd.grad.clone()))
+    for k, what in enumerate(("log_prob", "ref log_prob", "kl / behaviour / entropy", "d means", "d stds")):
+        _close(outs[0][k], outs[1][k], 3e-6, what)
