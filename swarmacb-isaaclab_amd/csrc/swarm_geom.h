@@ -7,6 +7,11 @@
 #pragma once
 #include <stdint.h>
 
+// Margin of the step kernel's wave-uniform wall-face mask (swarm_step_impl.h, SWARM_WALL_MASK)
+#ifndef SWARM_WALL_MARGIN
+#define SWARM_WALL_MARGIN 0.02f
+#endif
+
 namespace swarm {
 
 enum Mission : int32_t { DIRGATE = 0, XOR = 1, HOMING = 2, FORAGING = 3, SHELTERING = 4 };
@@ -45,6 +50,7 @@ enum RngPurpose : uint32_t {
     S(float, wall_clear_dg) /* r + 0.5*t + eps (DG:1050-1054) */                                             \
     /* kernel pre-filters only: face offsets -(p.n), radii inside which no face is within reach */            \
     A(float, face_d, 12) S(float, wall_safe_r2) S(float, ins_safe_r2)                                       \
+    S(float, wall_mask_r2) /* |p|^2 below it: no face within clearance + SWARM_WALL_MARGIN (step kernel) */    \
     S(float, wall_clear_mc) /* r (MC:533) */                                                                 \
     /* internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 */                                      \
     A(float, iw_nx, 3) A(float, iw_ny, 3) A(float, iw_ax, 3) A(float, iw_ay, 3) A(float, iw_tx, 3)          \

@@ -79,6 +79,8 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     }
     const double rs = apo - g.wall_clear_dg - 1e-4, ri = apo - 1e-3 - 1e-4;
     g.wall_safe_r2 = (float)(rs * rs);
+    const double rm = rs - (double)SWARM_WALL_MARGIN;
+    g.wall_mask_r2 = (float)(rm * rm);
     g.ins_safe_r2 = (float)(ri * ri);
 
     // mission zones (DG:649-656, DGC:163-167; SH:24-27 / MC:322-329)

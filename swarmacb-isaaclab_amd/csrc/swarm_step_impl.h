@@ -117,6 +117,16 @@
 #define SWARM_RAY_PREFILTER 0
 #endif
 
+// 1: the arena-wall pushes of one solver call test only the faces some robot of the wave was
+// within clearance + SWARM_WALL_MARGIN of when the call began (one wave-uniform face mask,
+// rebuilt if any robot has since moved farther than the margin): a face outside it is farther
+// than the clearance from every robot, i.e. it would add pen = 0 (a +-0 term). The faces are
+// then walked with scalar bit tests instead of a vector test + branch per face per call.
+// Bitwise-neutral.
+#ifndef SWARM_WALL_MASK
+#define SWARM_WALL_MASK 0
+#endif
+
 // 1: the contact solver's pair term from one hardware reciprocal square root
 // (dist = s * rsq(s), the normal d * rsq(s)) instead of a correctly rounded sqrt
 // and a reciprocal of dist + 1e-8: the same formula within ~2 ulp of dist, i.e.
@@ -481,6 +491,53 @@ __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
     y = y + ty;
 }
 
+// Wave-uniform mask of the arena faces a walls_dg call may need (SWARM_WALL_MASK): face k is in
+// it if some robot's fused signed-distance estimate was below clearance + 1e-4 + margin at
+// (x0, y0); while no robot has moved margin away from (x0, y0) since, a face outside the mask
+// still has sd >= clearance + 1e-4 for every robot (|n_k| = 1), i.e. walls_dg's own per-face
+// filter would skip it.
+struct WallMask {
+    uint32_t faces;   // wave-uniform
+    float x0, y0;
+};
+
+__device__ __forceinline__ void wall_mask_build(const Geom& g, WallMask& w, float x, float y) {
+    uint32_t m = 0;
+    if (__any(fmaf(x, x, y * y) >= g.wall_mask_r2)) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            const float sda = fmaf(x, g.face_nx[k], fmaf(y, g.face_ny[k], g.face_d[k]));
+            if (__any(sda < g.wall_clear_dg + 1e-4f + SWARM_WALL_MARGIN)) m |= 1u << k;
+        }
+    }
+    w.faces = m;
+    w.x0 = x;
+    w.y0 = y;
+}
+
+// walls_dg (DG:1048-1078) over the faces of a WallMask: the same terms in the same face order
+// (the skipped faces would add +-0); rebuilds the mask first if a robot left its margin
+__device__ __forceinline__ void walls_dg_masked(const Geom& g, WallMask& w, float& x, float& y) {
+    if (SWARM_ABLATE & 8) return;
+    const float dx = x - w.x0, dy = y - w.y0;
+    constexpr float lim = 0.999f * SWARM_WALL_MARGIN;
+    if (__any(dx * dx + dy * dy >= lim * lim)) wall_mask_build(g, w, x, y);
+    const uint32_t m = __builtin_amdgcn_readfirstlane(w.faces);
+    if (!m) return;   // no face within reach: every term is +-0 and x + 0 = x
+    float tx = 0.0f, ty = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        if (m & (1u << k)) {
+            const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
+            const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
+            tx += pen * g.face_nx[k];
+            ty += pen * g.face_ny[k];
+        }
+    }
+    x = x + tx;
+    y = y + ty;
+}
+
 // MC:531-553 — sequential per face with the robot radius as clearance.
 __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 #pragma unroll
@@ -722,7 +779,14 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     constexpr bool apply = APPLY;
-    walls_dg(g, x, y);
+#if SWARM_WALL_MASK
+    WallMask wmask;
+    wall_mask_build(g, wmask, x, y);
+#define SOLVE_WALLS(g, x, y) walls_dg_masked(g, wmask, x, y)
+#else
+#define SOLVE_WALLS(g, x, y) walls_dg(g, x, y)
+#endif
+    SOLVE_WALLS(g, x, y);
     if constexpr (INTERNAL) {
         if (!apply) capsules(g, x, y, false, 0.0f, 0.0f);
     }
@@ -735,7 +799,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
         const float bx = x, by = y;
         bool pushed = false;
         if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
-        walls_dg(g, x, y);
+        SOLVE_WALLS(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
             if (edge && !apply) {

@@ -17,10 +17,10 @@ for rep in 1 2; do
     python3 -c "import json; d=json.loads(open('$OUT/var_${name}_$rep.log').read().strip().splitlines()[-1]); print('$name rep $rep', 'value %.4g' % d['value'], 'kernel_us %.2f' % d['roofline']['kernel_avg_us'])"
   done
 done
-if [ -f build/variants/lib_all5.so ]; then
-  SWARMSTEP_LIB=$PWD/build/variants/lib_all5.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_philox.py \
-    -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_all5.log 2>&1
-  echo "all5 parity rc=$?"; tail -3 $OUT/pytest_all5.log
+if [ -f build/variants/lib_all6.so ]; then
+  SWARMSTEP_LIB=$PWD/build/variants/lib_all6.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_philox.py \
+    -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_all6.log 2>&1
+  echo "all6 parity rc=$?"; tail -3 $OUT/pytest_all6.log
 fi
 timeout -k 10 900 python3 -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread \
   > $OUT/pytest_gpu.log 2>&1
