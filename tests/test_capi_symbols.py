@@ -19,7 +19,7 @@ HEADERS = {"swarmstep.h": _native.EXPORTS, "swarmrollout.h": _native.ROLLOUT_EXP
 def declared_functions(header: str = "swarmstep.h") -> list[str]:
     text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(swarm_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(swarm_[a-z0-9_]+)\s*\(", text)))
 
 
 @pytest.mark.parametrize("header", sorted(HEADERS))

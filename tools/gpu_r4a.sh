@@ -11,6 +11,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4a
 for rep in 1 2; do
   for lib in build/variants/lib_*.so; do
+    [ -e "$lib" ] || continue
     name=$(basename $lib .so); name=${name#lib_}
     SWARMSTEP_LIB=$PWD/$lib timeout -k 10 120 python3 bench.py --cpu-seconds 0 --steps 600 --graph 0 > $OUT/var_${name}_$rep.log 2>&1 \
       || { echo "$name failed"; tail -5 $OUT/var_${name}_$rep.log; exit 2; }
