@@ -20,6 +20,7 @@ data path; value = all agent-steps / max-over-ranks time.
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
 import math
 import os
@@ -56,9 +57,12 @@ def parse():
     ap.add_argument("--prewarm", type=float, default=1.0,
                     help="seconds of untimed step launches on the timed engine before the warm-up "
                          "(steady clocks, arenas past the post-spawn contact burst; steps/warmup unchanged)")
-    ap.add_argument("--graph", type=int, default=1,
-                    help="1: the timed decisions are captured once as a HIP graph (with timing events as graph "
-                         "nodes at both ends) and replayed inside the timed region; 0: eager launches")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: the timed decisions are captured once as a HIP graph and replayed inside the "
+                         "timed region; 0: eager launches")
+    ap.add_argument("--gate", type=int, default=1,
+                    help="1: the timed launches are enqueued behind a stream gate released after the enqueue "
+                         "(swarm_gate_wait); 0: launched as they are enqueued")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
@@ -230,6 +234,7 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    from SwarmACB_isaac import _native
     from SwarmACB_isaac.engine import SwarmEngine
     from SwarmACB_isaac.shard import EnvShard, max_over_ranks
 
@@ -256,41 +261,49 @@ def main():
     # its own in the stream, and a pair per decision added ~5 us of GPU-side gap per launch);
     # the per-launch average includes the gaps between back-to-back launches, so it is an
     # upper bound on the kernel's own duration.
-    # --graph 1 (default): the n_dec timed launches are captured ONCE (nothing executes during
-    # capture; the engine's host state - Philox tick, episode-length mirror - advances exactly as
-    # the eager loop would) as one HIP graph whose first and last nodes are the two timing
-    # events, and the graph is replayed once inside the timed region. The events then see only
-    # the GPU's own work: with few timed launches (the driver's 4) eager events also counted
-    # the host's launch latency after the first event (BENCH_r03: 68.3 vs 59.5 us rocprofv3).
-    # The value stays wall-clock around the replay.
+    # --gate 1 (default): the timed region is enqueued behind a stream gate (swarm_gate_wait: a
+    # one-wave kernel that waits for a host-coherent flag) and released after the enqueue, so
+    # the launches run back to back from the release on and the events see only the GPU's own
+    # work; with few timed launches (the driver's 4) eager events otherwise also counted the
+    # host's launch latency after the first event (BENCH_r03: 68.3 vs 59.5 us rocprofv3). The
+    # wall clock starts at the release and stops after the synchronize: exactly the K steps.
+    # --graph 1: the timed decisions are captured once as a HIP graph and replayed behind the
+    # gate (the timing events stay outside the capture: ROCm refuses external events in one).
     stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     graph = None
     if args.graph:
-        ev0 = torch.cuda.Event(enable_timing=True, external=True)
-        ev1 = torch.cuda.Event(enable_timing=True, external=True)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            ev0.record()
             for d in range(n_dec):
                 eng.step(acts[n_warm + d], dp, out=out)
-            ev1.record()
-    else:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gate = None
+    if args.gate:
+        gate = C.c_void_p()
+        _native.check(eng.lib.swarm_gate_alloc(C.byref(gate)), "swarm_gate_alloc")
+        flag = C.c_uint32.from_address(gate.value)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
+    if gate is not None:
+        flag.value = 0
+        _native.check(eng.lib.swarm_gate_wait(gate, 10_000_000, C.c_void_p(stream.cuda_stream)), "swarm_gate_wait")
+    ev0.record(stream)
     if graph is not None:
         graph.replay()
     else:
-        ev0.record(stream)
         for d in range(n_dec):
             eng.step(acts[n_warm + d], dp, out=out)
-        ev1.record(stream)
+    ev1.record(stream)
+    t0 = time.perf_counter()
+    if gate is not None:
+        flag.value = 1
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if gate is not None:
+        _native.check(eng.lib.swarm_gate_free(gate), "swarm_gate_free")
     avg_kernel_s = ev0.elapsed_time(ev1) / n_dec / 1e3
     elapsed = max_over_ranks(elapsed, dev)
     total_agent_steps = world * E * N_AGENTS * steps
@@ -332,8 +345,9 @@ def main():
                 "global_envs": world * E,
                 "decision_period": dp,
                 "layout": args.layout or "default",
-                "timed_launches": "one HIP graph of the timed decisions, replayed once" if graph is not None
-                                  else "eager launches",
+                "timed_launches": ("one HIP graph of the timed decisions, replayed once" if graph is not None
+                                   else "eager launches") + (", enqueued behind a stream gate released after the "
+                                                             "enqueue" if gate is not None else ""),
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,
             },

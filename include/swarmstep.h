@@ -166,6 +166,14 @@ int64_t swarm_tick(const swarm_handle_t* h);
  * time-out flags, so it is 0 for every env when no bit is set). */
 int64_t swarm_last_timeouts(const swarm_handle_t* h);
 
+/* Measurement helpers (no reference counterpart; bench.py): a stream gate. swarm_gate_alloc
+ * returns a host-coherent flag word (0); swarm_gate_wait enqueues a one-wave kernel on `stream`
+ * that returns once the host has set *flag nonzero, or after timeout_us (at most 60 s), so the
+ * launches enqueued behind it run back to back from the release on. swarm_gate_free releases it. */
+int32_t swarm_gate_alloc(uint32_t** flag);
+int32_t swarm_gate_free(uint32_t* flag);
+int32_t swarm_gate_wait(const uint32_t* flag, int64_t timeout_us, void* stream);
+
 /* Behaviour-FSM packing helpers (host). Unpacked fields follow
  * BehaviorModules (behavior_modules.py:141-153). */
 uint32_t swarm_fsm_pack(int32_t ex_state, int32_t ex_steps, float ex_dir,

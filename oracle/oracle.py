@@ -189,13 +189,17 @@ class OracleEnv:
 
 
 class libm_perturb:
-    """Context manager: every oracle cos/sin/atan2/exp result nudged by `ulps` ulp."""
+    """Context manager: every oracle cos/sin/atan2/exp result nudged by `ulps` ulp, or (with
+    `cos` given) sin results by `ulps`, cos results by `cos` and atan2/exp results by `other`."""
 
-    def __init__(self, ulps: int):
-        self.ulps = int(ulps)
+    def __init__(self, ulps: int, cos: int | None = None, other: int = 0):
+        self.ulps, self.cos, self.other = int(ulps), cos, int(other)
 
     def __enter__(self):
-        lib().or_set_libm_perturb(self.ulps)
+        if self.cos is None:
+            lib().or_set_libm_perturb(self.ulps)
+        else:
+            lib().or_set_libm_perturb3(self.ulps, int(self.cos), self.other)
         return self
 
     def __exit__(self, *exc):

@@ -162,17 +162,24 @@ static void build_geom(const or_cfg* c, geom* g) {
 /*  result nudged by +-g_lm_ulps ulp to measure how far a step's outputs can */
 /*  move under that freedom. 0 (the default) = plain libm.                   */
 /* ------------------------------------------------------------------------ */
-static int g_lm_ulps = 0;
-void or_set_libm_perturb(int ulps) { g_lm_ulps = ulps; }
-static inline float lm_nudge(float v) {
-    for (int k = 0; k < g_lm_ulps; k++) v = nextafterf(v, INFINITY);
-    for (int k = 0; k < -g_lm_ulps; k++) v = nextafterf(v, -INFINITY);
+/*  sin and cos can also be nudged independently (or_set_libm_perturb3): two  */
+/*  implementations' sincos may round the pair in opposite directions.       */
+static int g_lm_sin = 0, g_lm_cos = 0, g_lm_other = 0;
+void or_set_libm_perturb(int ulps) { g_lm_sin = g_lm_cos = g_lm_other = ulps; }
+void or_set_libm_perturb3(int sin_ulps, int cos_ulps, int other_ulps) {
+    g_lm_sin = sin_ulps;
+    g_lm_cos = cos_ulps;
+    g_lm_other = other_ulps;
+}
+static inline float lm_nudge(float v, int ulps) {
+    for (int k = 0; k < ulps; k++) v = nextafterf(v, INFINITY);
+    for (int k = 0; k < -ulps; k++) v = nextafterf(v, -INFINITY);
     return v;
 }
-static inline float lm_cos(float a) { return lm_nudge(cosf(a)); }
-static inline float lm_sin(float a) { return lm_nudge(sinf(a)); }
-static inline float lm_atan2(float y, float x) { return lm_nudge(atan2f(y, x)); }
-static inline float lm_exp(float a) { return lm_nudge(expf(a)); }
+static inline float lm_cos(float a) { return lm_nudge(cosf(a), g_lm_cos); }
+static inline float lm_sin(float a) { return lm_nudge(sinf(a), g_lm_sin); }
+static inline float lm_atan2(float y, float x) { return lm_nudge(atan2f(y, x), g_lm_other); }
+static inline float lm_exp(float a) { return lm_nudge(expf(a), g_lm_other); }
 
 /* physical constants (DGC:122-137, 179; MC:118-121, 185-189) */
 #define R_ROBOT 0.035

@@ -90,6 +90,7 @@ void or_critic_state(const or_cfg* cfg, const float* pos, const float* yaw, floa
 
 /* Nudge every cos/sin/atan2/exp result by `ulps` ulp (0 = off): conditioning probe for tests. */
 void or_set_libm_perturb(int ulps);
+void or_set_libm_perturb3(int sin_ulps, int cos_ulps, int other_ulps);
 
 /* The production HIP kernel's Philox draws for one tick, laid out like or_draws
  * (rab (E,N,N); turns (3,E,N); isaac spawn (spawn_k,E,N,2) + yaw (E,N);

@@ -52,6 +52,7 @@ EXPORTS = [
     "swarm_abi_version", "swarm_strerror", "swarm_last_hip_error", "swarm_create", "swarm_destroy",
     "swarm_reset", "swarm_step", "swarm_critic_state", "swarm_sync_episode_lengths", "swarm_tick",
     "swarm_last_timeouts", "swarm_set_step_groups",
+    "swarm_gate_alloc", "swarm_gate_free", "swarm_gate_wait",
     "swarm_fsm_pack",
 ]
 
@@ -179,6 +180,12 @@ def load() -> C.CDLL:
     lib.swarm_rsa_attn_forward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp]
     lib.swarm_rsa_attn_backward.restype = i32
     lib.swarm_rsa_attn_backward.argtypes = [C.c_int64, i32, i32, i32, vp, vp, vp, vp, vp]
+    lib.swarm_gate_alloc.restype = i32
+    lib.swarm_gate_alloc.argtypes = [vp]
+    lib.swarm_gate_free.restype = i32
+    lib.swarm_gate_free.argtypes = [vp]
+    lib.swarm_gate_wait.restype = i32
+    lib.swarm_gate_wait.argtypes = [vp, C.c_int64, vp]
     lib.swarm_tensor_list_copy.restype = i32
     lib.swarm_tensor_list_copy.argtypes = [i32, vp, vp, vp, C.c_int64, vp, vp]
     lib.swarm_row_norm_forward.restype = i32

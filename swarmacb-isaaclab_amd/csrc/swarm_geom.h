@@ -5,6 +5,7 @@
 // or a torch.tensor(..., float32) table, and passed to the kernel by value
 // (kernarg segment -> scalar loads; every field is wave-uniform).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 // Margin of the step kernel's wave-uniform wall-face mask (swarm_step_impl.h, SWARM_WALL_MASK)
@@ -39,6 +40,10 @@ enum RngPurpose : uint32_t {
     S(uint32_t, seed_lo) S(uint32_t, seed_hi) S(uint32_t, env_off_lo) S(uint32_t, env_off_hi)               \
     S(int32_t, env0)     /* first arena of this step launch (env groups on separate streams, swarm_capi.cpp) */ \
     S(int32_t, env_n)    /* arenas of this step launch (0 = all E) */                                        \
+    /* arena order (SWARM_ARENA_ORDER, swarm_step_impl.h): buffer address (0 = identity order), the     */   \
+    /* set read by this launch (0-2), its tag, and the cost classes (wave life in 1024-clock units)     */   \
+    S(uint32_t, order_lo) S(uint32_t, order_hi) S(int32_t, order_set) S(int32_t, order_tag)                 \
+    S(int32_t, order_c0) S(int32_t, order_cw)                                                               \
     /* ---- mission constants (compile time in the kernels) ---- */                                          \
     S(int32_t, nseg) S(int32_t, nint) /* raycast segments (arena 12 + internal), internal walls */           \
     S(int32_t, has_light)                                                                                   \
@@ -75,6 +80,12 @@ enum RngPurpose : uint32_t {
     S(float, prox_range) S(float, rab_range) S(float, rab_loss) S(float, unity) S(float, light_thr)         \
     S(float, light_int) S(float, alpha) S(float, prox_thr) S(float, pi_f) S(float, two_pi_f)                \
     S(float, half_pi_f) S(float, critic_radius)
+
+// arena-order buffer of one handle (swarm_step_impl.h order_arena): 3 sets of kOrderHdr header
+// words + kOrderClasses lists of E local arena indices
+constexpr int kOrderClasses = 8;
+constexpr int kOrderHdr = 16;
+constexpr size_t order_set_words(int E) { return (size_t)kOrderHdr + (size_t)kOrderClasses * (size_t)E; }
 
 struct Geom {
 #define SWARM_GEOM_S(t, n) t n;

@@ -9,7 +9,7 @@
 // the W_hh^T slice it needs in registers and walks the steps in reverse. A
 // minibatch of the ML-Agents trainers (16 sequences x 128 steps) is then one
 // launch instead of 128 library LSTM calls (forward) plus 128 (backward).
-// Precise expf / tanhf: the results match torch.nn.LSTM to fp32 rounding.
+// Activations within a few ulp relative error (act_sigmoid / act_tanh, tanhf in the backward).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -66,13 +66,25 @@ __device__ __forceinline__ int batch_item(const Batch<S>& bt, int blk) {
 }
 __device__ float g_keep_one[1] = {1.0f};
 
-// Activations from the hardware exponential and reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp
-// each) instead of the library's expf / tanhf / IEEE division, which dominated the
-// per-step chain; tanh(x) = 2 sigmoid(2x) - 1 (absolute error ~1e-7 near 0).
-__device__ __forceinline__ float fast_sigmoid(float x) {
-    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+// Activations within a few ulp RELATIVE error everywhere, without the library's IEEE
+// division and tanhf expansion on the per-step chain: sigmoid = rcp(1 + expf(-x)) (library
+// expf, hardware reciprocal); tanh from 1 - 2 / (exp(2|x|) + 1) where |tanh| >= 0.55 and the
+// odd minimax polynomial of single-precision tanh (x + x^3 P(x^2), |x| < 0.625) below it, so
+// small gate values and cell outputs keep their relative accuracy. (The earlier
+// 2 sigmoid(2x) - 1 had an ABSOLUTE error of ~1e-7: relative 1e-4 at 1e-3, which 128-step
+// recurrences carried into the weight gradients; tests/test_gpu_lstm_seq.py, the L128
+// trainer fixtures.)
+__device__ __forceinline__ float act_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + expf(-x)); }
+__device__ __forceinline__ float act_tanh(float x) {
+    const float ax = fabsf(x);
+    const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * ax);        // exp(2|x|)
+    const float big = 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
+    const float z = x * x;
+    const float p = fmaf(fmaf(fmaf(fmaf(-5.70498872745e-3f, z, 2.06390887954e-2f), z, -5.37397155531e-2f), z,
+                              1.33314422036e-1f), z, -3.33332819422e-1f);
+    const float small = fmaf(p * z, ax, ax);
+    return copysignf(ax < 0.625f ? small : big, x);
 }
-__device__ __forceinline__ float fast_tanh(float x) { return 2.0f * fast_sigmoid(2.0f * x) - 1.0f; }
 
 // lane k's value of v, in a scalar register (v_readlane_b32 on the bit pattern)
 __device__ __forceinline__ float lane_bcast(float v, int k) {
@@ -149,7 +161,11 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
                 if (k + 3 < KU) a3 = fmaf(w[k + 3], hk[k + 3], a3);
             }
             const float a = ((a0 + a1) + (a2 + a3)) + xr[p];
-            const float v = kind == 2 ? fast_tanh(a) : fast_sigmoid(a);
+            float v;
+            if (kind == 2)   // wave-uniform for 64 units (wave q = gate q)
+                v = act_tanh(a);
+            else
+                v = act_sigmoid(a);
             if (row_j) {
                 g[j] = v;
                 act[row * G + j] = v;
@@ -157,7 +173,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
             __syncthreads();
             if (unit) {
                 c = g[U + lane] * c + g[lane] * g[2 * U + lane];
-                h = g[3 * U + lane] * fast_tanh(c);
+                h = g[3 * U + lane] * act_tanh(c);
                 if (wave == 0) {
                     h_out[row * U + lane] = h;
                     c_out[row * U + lane] = c;

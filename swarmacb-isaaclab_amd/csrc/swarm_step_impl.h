@@ -135,6 +135,15 @@
 #define SWARM_PAIR_RSQ 0
 #endif
 
+// 1: arenas are handed to the workgroups of a layout-103 launch heaviest first. Each wave of a
+// launch files its arena under a cost class (its own life in shader clocks) in an order buffer
+// owned by the handle; the next launch gives block b the b-th arena of that order, so the
+// arenas that set the launch's length start first, one per SIMD, as the oldest wave there
+// (VALU issue goes by priority, then age). Scheduling only: every arena's arithmetic is the
+// same, so results are bitwise unchanged. See order_arena() for the set rotation and checks.
+#ifndef SWARM_ARENA_ORDER
+#define SWARM_ARENA_ORDER 0
+#endif
 
 namespace swarm {
 
@@ -1604,10 +1613,69 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 // ---------------------------------------------------------------------------
 //  The fused step kernel
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+//  Arena order (SWARM_ARENA_ORDER). Buffer: 3 sets of kOrderHdr header words + kOrderClasses
+//  lists of E local arena indices. Launch t reads set R = order_set, appends to W = R + 1 and
+//  clears X = R + 2 (mod 3), so a set is cleared, filled by one launch and read by the next.
+//  Header: [0, 8) class counts, [8] env0, [9] arenas of the writing launch, [10] its tag.
+//  A set is used only if its counts sum to this launch's arena count and its env0 / count /
+//  tag (writer = reader tag - 1) match; otherwise block b takes arena b. Appends past the
+//  arena count are dropped, so every used set is a permutation of the launch's arenas even
+//  under graph replays of captured launches (which repeat their tags).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t* order_buf(const Geom& gr) {
+    return reinterpret_cast<int32_t*>(((uint64_t)gr.order_hi << 32) | gr.order_lo);
+}
+
+// local arena (0 .. nblk-1) of block b
+__device__ __forceinline__ int order_arena(const Geom& gr, int nblk, int b) {
+    const int32_t* h = order_buf(gr) + (size_t)gr.order_set * order_set_words(gr.E);
+    int cnt[kOrderClasses], sum = 0;
+#pragma unroll
+    for (int c = 0; c < kOrderClasses; ++c) {
+        cnt[c] = __builtin_amdgcn_readfirstlane(h[c]);
+        sum += cnt[c];
+    }
+    const bool ok = sum == nblk && __builtin_amdgcn_readfirstlane(h[8]) == gr.env0 &&
+                    __builtin_amdgcn_readfirstlane(h[9]) == nblk &&
+                    __builtin_amdgcn_readfirstlane(h[10]) == gr.order_tag - 1;
+    if (!ok) return b;
+    int o = b;
+#pragma unroll
+    for (int c = kOrderClasses - 1; c >= 0; --c) {   // heaviest class first
+        if (o < cnt[c]) {
+            const int a = __builtin_amdgcn_readfirstlane(h[kOrderHdr + (size_t)c * gr.E + o]);
+            return (a >= 0 && a < nblk) ? a : b;
+        }
+        o -= cnt[c];
+    }
+    return b;
+}
+
+// file this wave's arena under the class of its life (clocks) for the next launch
+__device__ __forceinline__ void order_file(const Geom& gr, int nblk, int arena, uint64_t life) {
+    int32_t* base = order_buf(gr);
+    const size_t sw = order_set_words(gr.E);
+    int32_t* w = base + (size_t)((gr.order_set + 1) % 3) * sw;
+    int32_t* x = base + (size_t)((gr.order_set + 2) % 3) * sw;
+    const int k = (int)(life >> 10) - gr.order_c0;
+    const int c = k < 0 ? 0 : min(kOrderClasses - 1, k / max(1, gr.order_cw));
+    if (threadIdx.x == 0) {
+        const int pos = atomicAdd(&w[c], 1);
+        if (pos < nblk) w[kOrderHdr + (size_t)c * gr.E + pos] = arena;
+        if (blockIdx.x == 0) {
+            w[8] = gr.env0;
+            w[9] = nblk;
+            w[10] = gr.order_tag;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < kOrderHdr) x[threadIdx.x] = 0;
+}
+
 // NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
 // every neighbour loop has a compile-time trip count and is fully unrolled.
 template <int NA, int LY>
-__device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime kernel argument
+__device__ __forceinline__ Lane make_lane(const Geom& g, int blk) {   // g: the runtime kernel argument
     constexpr int KL = ly_lanes(LY), P = ly_parts(LY);
     Lane L;
     L.N = NA > 0 ? NA : g.N;
@@ -1637,7 +1705,7 @@ __device__ __forceinline__ Lane make_lane(const Geom& g) {   // g: the runtime k
     const int chunk = (L.N + P - 1) / P;
     L.j0 = L.p * chunk;
     L.j1 = min(L.N, L.j0 + chunk);
-    L.env = g.env0 + (int)blockIdx.x * apb + L.a;
+    L.env = g.env0 + blk * apb + L.a;
     L.valid = (L.a < apb) && (L.env < g.E);
     L.ab = (L.a < apb ? L.a : 0) * L.N;
     // lanes beyond the last whole arena own no robot: park their tile writes in
@@ -1677,7 +1745,15 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     const Geom& g = kGeomTab[MISSION][PROFILE];   // mission constants as literals; gr: runtime fields
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
-    const Lane L = make_lane<NA, LY>(gr);
+    int blk = (int)blockIdx.x;
+#if SWARM_ARENA_ORDER
+    constexpr bool ORDERED = !REPLAY && LY == 103;
+    const int nblk = gr.env_n > 0 ? gr.env_n : gr.E;
+    const bool ordered = ORDERED && (gr.order_lo | gr.order_hi) != 0;
+    const uint64_t ord_t0 = __builtin_amdgcn_s_memtime();
+    if (ordered) blk = order_arena(gr, nblk, blk);
+#endif
+    const Lane L = make_lane<NA, LY>(gr, blk);
     stage_tables<LY>(g, S);
     // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
     const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
@@ -1859,6 +1935,9 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
         }
     }
+#if SWARM_ARENA_ORDER
+    if (ordered) order_file(gr, nblk, blk, __builtin_amdgcn_s_memtime() - ord_t0);
+#endif
 #if SWARM_WAVE_TIMING
     if constexpr (!REPLAY && ly_waves(LY) == 1) {
         const uint64_t wt_c1 = __builtin_amdgcn_s_memtime();
@@ -1899,7 +1978,7 @@ __global__ __launch_bounds__(64) void reset_kernel(const Geom gr, const DevState
     constexpr int C = NA > 0 ? NA : 0;
     const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY> S;
-    const Lane L = make_lane<NA, LY>(gr);
+    const Lane L = make_lane<NA, LY>(gr, (int)blockIdx.x);
     stage_tables<LY>(g, S);
     const size_t q = L.valid ? (size_t)L.env * L.N + L.i : 0;
     const size_t EN = (size_t)L.E * L.N;

@@ -1,4 +1,5 @@
-// swarm_util.hip — multi-tensor copy for the trainers' graphed steps (include/swarmtrain.h).
+// swarm_util.hip — multi-tensor copy for the trainers' graphed steps (include/swarmtrain.h), and
+// the stream gate of the benchmarks (include/swarmstep.h).
 //
 // The OC2 update keeps or undoes each minibatch's actor Adam step on a device
 // predicate (its KL early stop, learned_option_critic_trainer.py:1421-1660): the
@@ -30,7 +31,40 @@ __global__ __launch_bounds__(kThreads) void list_copy_kernel(const uint64_t* __r
         d[i] = s[i];
 }
 
+// Stream gate: one lane polls a host-coherent word until the host sets it (or the wall clock,
+// 100 MHz, passes the limit: every launch of it ends), so the work enqueued behind it runs
+// back to back from the release on, without the host's launch latency in between.
+__global__ __launch_bounds__(64) void gate_kernel(const uint32_t* flag, uint64_t limit_ticks) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit_ticks) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
 }  // namespace
+
+extern "C" int32_t swarm_gate_alloc(uint32_t** flag) {
+    if (!flag) return SWARM_ERR_ARG;
+    *flag = nullptr;
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return SWARM_ERR_HIP;
+    *static_cast<volatile uint32_t*>(p) = 0u;
+    *flag = static_cast<uint32_t*>(p);
+    return SWARM_OK;
+}
+
+extern "C" int32_t swarm_gate_free(uint32_t* flag) {
+    if (!flag) return SWARM_ERR_ARG;
+    return hipHostFree(flag) == hipSuccess ? SWARM_OK : SWARM_ERR_HIP;
+}
+
+extern "C" int32_t swarm_gate_wait(const uint32_t* flag, int64_t timeout_us, void* stream) {
+    if (!flag || timeout_us < 0 || timeout_us > 60000000) return SWARM_ERR_ARG;
+    hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, (uint64_t)timeout_us * 100u);
+    return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP;
+}
 
 extern "C" int32_t swarm_tensor_list_copy(int32_t n, const uint64_t* dst_ptrs, const uint64_t* src_ptrs,
                                           const int64_t* words, int64_t max_words, const uint8_t* unless,

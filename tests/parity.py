@@ -10,7 +10,8 @@ Tolerance (stated once, used by every parity test):
     bearing terms is as accurate as the sum, not as its own value) — and
     `spread` is how far the oracle's own output moves when its inputs are
     perturbed by one ulp (yaw +-1 ulp, positions +-1 ulp) or when every
-    cos/sin/atan2/exp result inside the step is nudged by +-1 ulp. The
+    cos/sin/atan2/exp result inside the step is nudged by +-1 ulp, or the sin
+    and cos results alone, each or both in either direction. The
     reference evaluates those with SLEEF on the CPU; any other implementation
     (glibc here, ocml on the GPU) differs by about 1 ulp, and near-tangent IR
     rays (ray-disc hits with r^2 - c^2 ~ 1e-7) / near-perpendicular light
@@ -139,19 +140,28 @@ def reference_after(fx, t: int) -> dict:
     return ref
 
 
-PERTURBATIONS = ("yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-")
+PERTURBATIONS = ("yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-", "sin+", "sin-", "cos+", "cos-", "sc+-", "sc-+")
+# libm nudges per perturbation: (sin, cos, atan2 / exp) ulps
+_LIBM = {"lm+": (1, 1, 1), "lm-": (-1, -1, -1), "sin+": (1, 0, 0), "sin-": (-1, 0, 0), "cos+": (0, 1, 0),
+         "cos-": (0, -1, 0), "sc+-": (1, -1, 0), "sc-+": (-1, 1, 0)}
+
+
+def perturbed_call(env, perturb: str | None, fn):
+    """fn() with one of PERTURBATIONS applied to env / the oracle's libm (None = plain)."""
+    if perturb in _LIBM:
+        s, c, o = _LIBM[perturb]
+        with O.libm_perturb(s, cos=c, other=o):
+            return fn()
+    if perturb:
+        what, sign = perturb[:-1], perturb[-1]
+        direction = np.inf if sign == "+" else -np.inf
+        env.s[what] = np.nextafter(env.s[what], np.float32(direction)).astype(np.float32)
+    return fn()
 
 
 def perturbed_step(env, perturb: str | None, **kw):
     """env.step(**kw) with one of PERTURBATIONS applied (None = plain)."""
-    if perturb:
-        what, sign = perturb[:-1], perturb[-1]
-        if what == "lm":
-            with O.libm_perturb(1 if sign == "+" else -1):
-                return env.step(**kw)
-        direction = np.inf if sign == "+" else -np.inf
-        env.s[what] = np.nextafter(env.s[what], np.float32(direction)).astype(np.float32)
-    return env.step(**kw)
+    return perturbed_call(env, perturb, lambda: env.step(**kw))
 
 
 def oracle_run(fx, t: int, perturb: str | None = None) -> dict:
@@ -423,17 +433,7 @@ def check_kernel_step(cfg: tuple, before: dict, actions, draws: dict, got: dict)
         env = O.OracleEnv(mission, profile, len(envs), N, obs_dim, discrete, max_len)
         env.load(state, prefix="")
         rab = np.ascontiguousarray(np.take(draws["rab_u_obs"], envs, axis=0))
-        if perturb:
-            what, sign = perturb[:-1], perturb[-1]
-            if what == "lm":
-                with O.libm_perturb(1 if sign == "+" else -1):
-                    obs = env.observe(rab)
-            else:
-                env.s[what] = np.nextafter(env.s[what], np.float32(np.inf if sign == "+" else -np.inf)).astype(
-                    np.float32)
-                obs = env.observe(rab)
-        else:
-            obs = env.observe(rab)
+        obs = perturbed_call(env, perturb, lambda: env.observe(rab))
         out = {"obs": obs}
         if profile == "isaac":
             out["cache"] = np.copy(env.s["cache"])

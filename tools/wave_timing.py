@@ -54,6 +54,8 @@ def main():
     torch.cuda.synchronize(dev)
     buf = np.zeros((E, 7, 4), np.uint32)
     rows = []
+    prev_life = prev_pred = None
+    prev_simd_end = prev_simd_key = None
     for d in range(300, 310):
         st = eng.dump_state()
         eng.step(acts[d], dp, out=out)
@@ -111,6 +113,36 @@ def main():
         pred = A @ coef
         rows[-1]["fit_us"] = dict(zip(["const"] + list(work), map(float, coef)))
         rows[-1]["fit_r2"] = float(1 - ((life_ns / 1e3 - pred) ** 2).sum() / ((life_ns / 1e3 - life_ns.mean() / 1e3) ** 2).sum())
+        # schedule view: which SIMD each block landed on, in what start order, and how far a
+        # SIMD's end follows the work of the four arenas it holds
+        start = w0 - t0
+        order = np.argsort(start, kind="stable")
+        rank = np.zeros(E, np.int64)
+        for s_ in range(cnt.size):
+            blk = np.nonzero(inv == s_)[0]
+            rank[blk[np.argsort(start[blk], kind="stable")]] = np.arange(blk.size)
+        first = np.arange(E) < cnt.size
+        rows[-1]["sched"] = {
+            "simds": int(cnt.size),
+            "distinct_simds_of_first_blocks": int(np.unique(inv[first]).size),
+            "rank_of_block_quarters": [np.bincount(rank[q * E // 4:(q + 1) * E // 4], minlength=4).tolist()
+                                       for q in range(4)],
+            "start_order_vs_block_corr": float(np.corrcoef(order, np.arange(E))[0, 1]),
+            "corr_simd_end_sum_life": float(np.corrcoef(simd_end, np.bincount(inv, life_ns))[0, 1]),
+            "corr_simd_end_max_life": float(np.corrcoef(simd_end, np.maximum.reduceat(
+                life_ns[np.argsort(inv, kind="stable")], np.r_[0, np.cumsum(cnt)[:-1]]))[0, 1]),
+        }
+        simd_key = np.unique(simd)
+        rows[-1]["sched"]["slowest_simd"] = int(simd_key[int(np.argmax(simd_end))])
+        rows[-1]["sched"]["simd_end_by_xcc_us"] = [round(float(simd_end[(simd_key >> 16) == x].mean() / 1e3), 2)
+                                                   for x in range(8)]
+        if prev_simd_end is not None and prev_simd_key.size == simd_key.size and (prev_simd_key == simd_key).all():
+            rows[-1]["sched"]["corr_simd_end_prev_launch"] = float(np.corrcoef(simd_end, prev_simd_end)[0, 1])
+        prev_simd_end, prev_simd_key = simd_end.copy(), simd_key
+        if prev_life is not None:
+            rows[-1]["sched"]["corr_life_prev_launch"] = float(np.corrcoef(life_ns, prev_life)[0, 1])
+            rows[-1]["sched"]["corr_pred_prev_launch"] = float(np.corrcoef(pred, prev_pred)[0, 1])
+        prev_life, prev_pred = life_ns.copy(), pred.copy()
         print(json.dumps(rows[-1]), flush=True)
     eng.close()
 
