@@ -27,12 +27,15 @@ import torch
 
 # SWARM_GRAPHS=0 forces eager steps
 ENABLED = os.environ.get("SWARM_GRAPHS", "1") != "0"
-# SWARM_GRAPHS_DIST=1 also captures multi-rank steps on the RCCL ("nccl") backend: the
-# flat-gradient all-reduce and the loss-denominator all-reduces go into the graph (RCCL
-# collectives are stream-ordered and capturable; gloo's host round trips are not). Off by
-# default: a captured collective cannot be validated without two GPUs (RCCL refuses two
-# ranks on one device), and a capture that fails falls back to eager steps anyway.
-DIST_ENABLED = os.environ.get("SWARM_GRAPHS_DIST", "0") == "1"
+# Multi-rank steps on the RCCL ("nccl") backend are captured too (SWARM_GRAPHS_DIST=0 keeps
+# them eager): the flat-gradient all-reduce and the loss-denominator all-reduces go into the
+# graph (RCCL collectives are stream-ordered and capturable; gloo's host round trips are not).
+# On by default since round 4: on MI355X a world-1 RCCL group running every collective of the
+# multi-rank update eagerly, then captured and replayed, gives the eager update bit for bit
+# (tests/test_gpu_rccl_graph.py; two ranks need two GPUs, which one process never gets here).
+# Every rank reports whether its steps were graphed (Trainer.step_path), and a capture that
+# fails falls back to eager steps, which issue the same collectives in the same order.
+DIST_ENABLED = os.environ.get("SWARM_GRAPHS_DIST", "1") != "0"
 
 
 def make_capturable(optimizers, device: torch.device):

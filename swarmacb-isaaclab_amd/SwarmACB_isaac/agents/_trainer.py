@@ -397,7 +397,7 @@ class TrainerBase:
     # ------------------------------------------------------------ graphed steps
     def _graphs_ok(self) -> bool:
         """Replay optimizer steps from a HIP graph (agents/_graph.py): a ROCm device, no
-        per-step test hooks, one process (or RCCL ranks with SWARM_GRAPHS_DIST=1)."""
+        per-step test hooks, one process or RCCL ranks (unless SWARM_GRAPHS_DIST=0)."""
         dist_ok = not self.comm.active or (_graph.DIST_ENABLED and self.comm.backend == "nccl")
         return (_graph.ENABLED and self.device.type == "cuda" and dist_ok
                 and self.grad_hook is None and self.step_hook is None)
