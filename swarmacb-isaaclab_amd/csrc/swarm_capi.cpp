@@ -79,7 +79,7 @@ struct swarm_handle {
     hipEvent_t gfork = nullptr;
     // arena order of layout-103 launches (SWARM_ARENA_ORDER in the kernels): 3 sets, see
     // swarm_step_impl.h order_arena(); allocated by the first swarm_reset
-    int32_t* d_order = nullptr;
+    uint32_t* d_order = nullptr;
     uint64_t order_launch = 0;
     bool order_on = true;
 };
@@ -165,9 +165,9 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
         }
     }
     // arena-order cost classes: wave life in 1024-clock units, class = (life - c0) / cw
-    h->g.order_c0 = env_int("SWARM_ORDER_C0", 40);
-    h->g.order_cw = env_int("SWARM_ORDER_CW", 10);
-    h->order_on = h->g.layout == 103 && env_int("SWARM_ORDER", 1) != 0;
+    h->g.order_c0 = env_int("SWARM_ORDER_C0", 50);
+    h->g.order_cw = env_int("SWARM_ORDER_CW", 8);
+    h->order_on = h->g.layout == 103 && p->num_envs <= kOrderMaxEnvs && env_int("SWARM_ORDER", 1) != 0;
     h->mirror.max_len = p->max_episode_length;
     h->lens.assign(p->num_envs, 0);
     h->mirror.assign(h->lens.data(), p->num_envs);
@@ -266,7 +266,7 @@ int32_t swarm_reset(swarm_handle_t* h, const swarm_state_t* state, const uint8_t
         h->lens_exact = true;
     }
     if (h->order_on && !h->d_order) {
-        const size_t bytes = 3 * order_set_words(E) * sizeof(int32_t);
+        const size_t bytes = order_buffer_words(E) * sizeof(uint32_t);
         if (hipMalloc(&h->d_order, bytes) != hipSuccess) {
             (void)hip_status();
             return SWARM_ERR_HIP;

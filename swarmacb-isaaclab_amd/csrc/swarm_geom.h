@@ -82,10 +82,20 @@ enum RngPurpose : uint32_t {
     S(float, half_pi_f) S(float, critic_radius)
 
 // arena-order buffer of one handle (swarm_step_impl.h order_arena): 3 sets of kOrderHdr header
-// words + kOrderClasses lists of E local arena indices
+// words + kOrderClasses bitmaps of order_wpc(E) words (padded so that each of the 64 lanes of
+// a wave reads a multiple of 4 words), then order_buffer_words - 3 sets = one float per arena
 constexpr int kOrderClasses = 8;
 constexpr int kOrderHdr = 16;
-constexpr size_t order_set_words(int E) { return (size_t)kOrderHdr + (size_t)kOrderClasses * (size_t)E; }
+constexpr int kOrderMaxEnvs = 16384;   // larger launches keep the identity order (scan cost)
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr int order_wpc(int E) { return ((((E + 31) >> 5) + 31) >> 5) << 5; }
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+constexpr size_t order_set_words(int E) { return (size_t)kOrderHdr + (size_t)kOrderClasses * (size_t)order_wpc(E); }
+constexpr size_t order_buffer_words(int E) { return 3 * order_set_words(E) + (size_t)E; }
 
 struct Geom {
 #define SWARM_GEOM_S(t, n) t n;

@@ -135,6 +135,14 @@
 #define SWARM_PAIR_RSQ 0
 #endif
 
+// 1: the contact solver's candidate loop takes a lane's candidates two at a time (the second
+// one's term computed as an independent chain and added, in increasing j, only if present), so
+// a lane with k candidates loops ceil(k / 2) times instead of k. Same terms in the same order:
+// bitwise-neutral.
+#ifndef SWARM_PAIR2
+#define SWARM_PAIR2 0
+#endif
+
 // 1: arenas are handed to the workgroups of a layout-103 launch heaviest first. Each wave of a
 // launch files its arena under a cost class (its own life in shader clocks) in an order buffer
 // owned by the handle; the next launch gives block b the b-th arena of that order, so the
@@ -601,16 +609,61 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         cx += row ? 0.0f : -hx;
         cy += row ? 0.0f : -hy;
     };
+    // pair_term's half-overlap push (hx, hy) of one pair without the branch: (+0, +0) when the
+    // pair does not overlap, which leaves the sums it is added to unchanged
+    auto pair_push = [&](int, float dx, float dy, float& hx, float& hy) {
+#if SWARM_PAIR_RSQ
+        const float s2 = fmaf(dx, dx, fmaf(dy, dy, 1e-8f));
+        const float rs = __builtin_amdgcn_rsqf(s2);
+        const float ov = fmaf(-s2, rs, g.min_dist);
+        const float hh = ov > 0.0f ? ov * rs * 0.5f : 0.0f;
+        hx = hh * dx;
+        hy = hh * dy;
+#else
+        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
+        const float ov = g.min_dist - dist;
+        const float inv = frcp(dist + 1e-8f);
+        const bool on = ov > 0.0f;
+        hx = on ? ov * (dx * inv) * 0.5f : 0.0f;
+        hy = on ? ov * (dy * inv) * 0.5f : 0.0f;
+#endif
+    };
+    (void)pair_push;
     if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
         const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
             return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
         });
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
+#if SWARM_PAIR2
+        uint32_t cm = cand;
+        while (cm) {
+            SWARM_WT(L.wt_pair++);
+            const int j1 = L.j0 + __builtin_ctz(cm);
+            cm &= cm - 1u;
+            const bool two = cm != 0u;
+            const int j2 = two ? L.j0 + __builtin_ctz(cm) : j1;
+            cm &= two ? cm - 1u : cm;
+            const float2 p1 = S.xy[L.ab + j1], p2 = S.xy[L.ab + j2];
+            float h1x, h1y, h2x, h2y;
+            pair_push(j1, x - p1.x, y - p1.y, h1x, h1y);
+            pair_push(j2, x - p2.x, y - p2.y, h2x, h2y);
+            const bool r1 = j1 > L.i, r2 = j2 > L.i;
+            rx += r1 ? h1x : 0.0f;
+            ry += r1 ? h1y : 0.0f;
+            cx += r1 ? 0.0f : -h1x;
+            cy += r1 ? 0.0f : -h1y;
+            rx += (two & r2) ? h2x : 0.0f;
+            ry += (two & r2) ? h2y : 0.0f;
+            cx += (two & !r2) ? -h2x : 0.0f;
+            cy += (two & !r2) ? -h2y : 0.0f;
+        }
+#else
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
             pair_term(j, x - p.x, y - p.y);
         });
+#endif
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
     } else {
         unsigned long long cand = 0;
@@ -1614,62 +1667,86 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 //  The fused step kernel
 // ---------------------------------------------------------------------------
 // ---------------------------------------------------------------------------
-//  Arena order (SWARM_ARENA_ORDER). Buffer: 3 sets of kOrderHdr header words + kOrderClasses
-//  lists of E local arena indices. Launch t reads set R = order_set, appends to W = R + 1 and
-//  clears X = R + 2 (mod 3), so a set is cleared, filled by one launch and read by the next.
-//  Header: [0, 8) class counts, [8] env0, [9] arenas of the writing launch, [10] its tag.
-//  A set is used only if its counts sum to this launch's arena count and its env0 / count /
-//  tag (writer = reader tag - 1) match; otherwise block b takes arena b. Appends past the
-//  arena count are dropped, so every used set is a permutation of the launch's arenas even
-//  under graph replays of captured launches (which repeat their tags).
+//  Arena order (SWARM_ARENA_ORDER). Buffer (swarm_geom.h order_set_words): 3 sets of
+//  kOrderHdr header words + kOrderClasses bitmaps of order_wpc(E) words (class slot 0 =
+//  heaviest), then one float per arena (its smoothed life). Launch t reads set R = order_set,
+//  files into W = R + 1 and clears X = R + 2 (mod 3): a set is cleared, filled by one launch
+//  and read by the next. Each wave of launch t sets its arena's bit in the bitmap of its cost
+//  class (one non-returning atomicOr); block b of launch t + 1 takes the b-th set bit in slot
+//  order. Header: [8] env0, [9] arenas of the writing launch, [10] its tag. A set is used only
+//  if its header matches this launch (env0, arena count, writer tag = reader tag - 1) and its
+//  bitmaps hold exactly as many bits as this launch has arenas (each filing wave sets one bit
+//  of its own arena, so the set is then a permutation; a set filed twice without a clear, as a
+//  graph replay of captured launches can do, either still is one or holds too many bits);
+//  otherwise block b takes arena b.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int32_t* order_buf(const Geom& gr) {
-    return reinterpret_cast<int32_t*>(((uint64_t)gr.order_hi << 32) | gr.order_lo);
+__device__ __forceinline__ uint32_t* order_buf(const Geom& gr) {
+    return reinterpret_cast<uint32_t*>(((uint64_t)gr.order_hi << 32) | gr.order_lo);
 }
 
 // local arena (0 .. nblk-1) of block b
 __device__ __forceinline__ int order_arena(const Geom& gr, int nblk, int b) {
-    const int32_t* h = order_buf(gr) + (size_t)gr.order_set * order_set_words(gr.E);
-    int cnt[kOrderClasses], sum = 0;
-#pragma unroll
-    for (int c = 0; c < kOrderClasses; ++c) {
-        cnt[c] = __builtin_amdgcn_readfirstlane(h[c]);
-        sum += cnt[c];
+    const int wpc = order_wpc(gr.E);
+    const uint32_t* h = order_buf(gr) + (size_t)gr.order_set * order_set_words(gr.E);
+    const bool hdr_ok = (int)__builtin_amdgcn_readfirstlane(h[8]) == gr.env0 &&
+                        (int)__builtin_amdgcn_readfirstlane(h[9]) == nblk &&
+                        (int)__builtin_amdgcn_readfirstlane(h[10]) == gr.order_tag - 1;
+    if (!hdr_ok) return b;
+    const int lane = threadIdx.x & 63;
+    const int per = wpc * kOrderClasses / 64;           // words per lane, a multiple of 4
+    const uint32_t* mine = h + kOrderHdr + (size_t)lane * per;
+    int cnt = 0;
+    for (int k = 0; k < per; k += 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(mine + k);
+        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
     }
-    const bool ok = sum == nblk && __builtin_amdgcn_readfirstlane(h[8]) == gr.env0 &&
-                    __builtin_amdgcn_readfirstlane(h[9]) == nblk &&
-                    __builtin_amdgcn_readfirstlane(h[10]) == gr.order_tag - 1;
-    if (!ok) return b;
-    int o = b;
+    int incl = cnt;   // inclusive prefix over the lanes
 #pragma unroll
-    for (int c = kOrderClasses - 1; c >= 0; --c) {   // heaviest class first
-        if (o < cnt[c]) {
-            const int a = __builtin_amdgcn_readfirstlane(h[kOrderHdr + (size_t)c * gr.E + o]);
-            return (a >= 0 && a < nblk) ? a : b;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(incl, d);
+        incl += lane >= d ? t : 0;
+    }
+    if (__builtin_amdgcn_readlane(incl, 63) != nblk) return b;
+    const int L = __ffsll((long long)__ballot(incl > b)) - 1;    // the lane holding set bit number b
+    int found = -1;
+    if (lane == L) {
+        int off = b - (incl - cnt);
+        for (int k = 0; k < per; ++k) {
+            uint32_t v = mine[k];
+            const int pc = __popc(v);
+            if (off < pc) {
+                for (; off > 0; --off) v &= v - 1u;
+                found = ((lane * per + k) % wpc) * 32 + __builtin_ctz(v);
+                break;
+            }
+            off -= pc;
         }
-        o -= cnt[c];
     }
-    return b;
+    found = __builtin_amdgcn_readlane(found, L);
+    return (found >= 0 && found < nblk) ? found : b;
 }
 
-// file this wave's arena under the class of its life (clocks) for the next launch
-__device__ __forceinline__ void order_file(const Geom& gr, int nblk, int arena, uint64_t life) {
-    int32_t* base = order_buf(gr);
+// file this wave's arena under the class of its smoothed life (1024-clock units) for the next
+// launch; block 0 also writes W's header and clears X
+__device__ __forceinline__ void order_file(const Geom& gr, int nblk, int arena, float ema) {
+    uint32_t* base = order_buf(gr);
     const size_t sw = order_set_words(gr.E);
-    int32_t* w = base + (size_t)((gr.order_set + 1) % 3) * sw;
-    int32_t* x = base + (size_t)((gr.order_set + 2) % 3) * sw;
-    const int k = (int)(life >> 10) - gr.order_c0;
+    const int wpc = order_wpc(gr.E);
+    uint32_t* w = base + (size_t)((gr.order_set + 1) % 3) * sw;
+    uint32_t* x = base + (size_t)((gr.order_set + 2) % 3) * sw;
+    const int k = (int)ema - gr.order_c0;
     const int c = k < 0 ? 0 : min(kOrderClasses - 1, k / max(1, gr.order_cw));
     if (threadIdx.x == 0) {
-        const int pos = atomicAdd(&w[c], 1);
-        if (pos < nblk) w[kOrderHdr + (size_t)c * gr.E + pos] = arena;
+        atomicOr(&w[kOrderHdr + (size_t)(kOrderClasses - 1 - c) * wpc + (arena >> 5)], 1u << (arena & 31));
+        reinterpret_cast<float*>(base + 3 * sw)[arena] = ema;
         if (blockIdx.x == 0) {
-            w[8] = gr.env0;
-            w[9] = nblk;
-            w[10] = gr.order_tag;
+            w[8] = (uint32_t)gr.env0;
+            w[9] = (uint32_t)nblk;
+            w[10] = (uint32_t)gr.order_tag;
         }
     }
-    if (blockIdx.x == 0 && threadIdx.x < kOrderHdr) x[threadIdx.x] = 0;
+    if (blockIdx.x == 0)
+        for (size_t i = threadIdx.x; i < sw; i += 64) x[i] = 0u;
 }
 
 // NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
@@ -1751,7 +1828,11 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     const int nblk = gr.env_n > 0 ? gr.env_n : gr.E;
     const bool ordered = ORDERED && (gr.order_lo | gr.order_hi) != 0;
     const uint64_t ord_t0 = __builtin_amdgcn_s_memtime();
-    if (ordered) blk = order_arena(gr, nblk, blk);
+    float ord_ema = 0.0f;
+    if (ordered) {
+        blk = order_arena(gr, nblk, blk);
+        ord_ema = reinterpret_cast<const float*>(order_buf(gr) + 3 * order_set_words(gr.E))[blk];
+    }
 #endif
     const Lane L = make_lane<NA, LY>(gr, blk);
     stage_tables<LY>(g, S);
@@ -1936,7 +2017,10 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         }
     }
 #if SWARM_ARENA_ORDER
-    if (ordered) order_file(gr, nblk, blk, __builtin_amdgcn_s_memtime() - ord_t0);
+    if (ordered) {
+        const float life = (float)((__builtin_amdgcn_s_memtime() - ord_t0) >> 10);
+        order_file(gr, nblk, blk, ord_ema > 0.0f ? 0.5f * (ord_ema + life) : life);
+    }
 #endif
 #if SWARM_WAVE_TIMING
     if constexpr (!REPLAY && ly_waves(LY) == 1) {
