@@ -10,7 +10,6 @@
 #include <cmath>
 #include <cstddef>
 #include <cstdint>
-#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
@@ -77,19 +76,9 @@ struct swarm_handle {
     hipStream_t gstream[SWARM_MAX_STEP_GROUPS] = {};
     hipEvent_t gjoin[SWARM_MAX_STEP_GROUPS] = {};
     hipEvent_t gfork = nullptr;
-    // arena order of layout-103 launches (SWARM_ARENA_ORDER in the kernels): 3 sets, see
-    // swarm_step_impl.h order_arena(); allocated by the first swarm_reset
-    uint32_t* d_order = nullptr;
-    uint64_t order_launch = 0;
-    bool order_on = true;
 };
 
 namespace {
-
-int env_int(const char* name, int dflt) {
-    const char* v = std::getenv(name);
-    return v && *v ? std::atoi(v) : dflt;
-}
 
 DevState dev_state(const swarm_state_t* s) {
     return DevState{s->pos_x, s->pos_y, s->yaw, s->fsm, s->wheel_l, s->wheel_r, s->sensor_cache, s->ground_prev,
@@ -164,10 +153,6 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
             return SWARM_ERR_ABI;
         }
     }
-    // arena-order cost classes: wave life in 1024-clock units, class = (life - c0) / cw
-    h->g.order_c0 = env_int("SWARM_ORDER_C0", 50);
-    h->g.order_cw = env_int("SWARM_ORDER_CW", 8);
-    h->order_on = h->g.layout == 103 && p->num_envs <= kOrderMaxEnvs && env_int("SWARM_ORDER", 1) != 0;
     h->mirror.max_len = p->max_episode_length;
     h->lens.assign(p->num_envs, 0);
     h->mirror.assign(h->lens.data(), p->num_envs);
@@ -210,7 +195,6 @@ int32_t swarm_destroy(swarm_handle_t* h) {
     if (!h) return SWARM_ERR_ARG;
     free_groups(h);
     if (h->d_mask) (void)hipFree(h->d_mask);
-    if (h->d_order) (void)hipFree(h->d_order);
     delete h;
     return SWARM_OK;
 }
@@ -265,14 +249,6 @@ int32_t swarm_reset(swarm_handle_t* h, const swarm_state_t* state, const uint8_t
         h->mirror.assign(h->lens.data(), E);
         h->lens_exact = true;
     }
-    if (h->order_on && !h->d_order) {
-        const size_t bytes = order_buffer_words(E) * sizeof(uint32_t);
-        if (hipMalloc(&h->d_order, bytes) != hipSuccess) {
-            (void)hip_status();
-            return SWARM_ERR_HIP;
-        }
-        if (hipMemsetAsync(h->d_order, 0, bytes, s) != hipSuccess) return hip_status();
-    }
     const DevState st = dev_state(state);
     const DevOut o{out->obs, out->reward, out->truncated};
     launch_reset(h->g, st, dmask, o, dev_replay(replay), h->tick, s);
@@ -314,16 +290,7 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
                 return hip_status();
         }
     } else {
-        Geom g = h->g;
-        if (h->d_order && !replay) {
-            const uint64_t a = (uint64_t)(uintptr_t)h->d_order;
-            g.order_lo = (uint32_t)a;
-            g.order_hi = (uint32_t)(a >> 32);
-            g.order_set = (int32_t)(h->order_launch % 3);
-            g.order_tag = (int32_t)(h->order_launch & 0x7fffffffu);
-            h->order_launch += 1;
-        }
-        launch_step(g, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any, cs);
+        launch_step(h->g, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any, cs);
     }
     h->tick += (uint64_t)n_substeps;
     return hip_status();

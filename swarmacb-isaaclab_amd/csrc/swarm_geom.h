@@ -5,13 +5,7 @@
 // or a torch.tensor(..., float32) table, and passed to the kernel by value
 // (kernarg segment -> scalar loads; every field is wave-uniform).
 #pragma once
-#include <stddef.h>
 #include <stdint.h>
-
-// Margin of the step kernel's wave-uniform wall-face mask (swarm_step_impl.h, SWARM_WALL_MASK)
-#ifndef SWARM_WALL_MARGIN
-#define SWARM_WALL_MARGIN 0.02f
-#endif
 
 namespace swarm {
 
@@ -40,10 +34,6 @@ enum RngPurpose : uint32_t {
     S(uint32_t, seed_lo) S(uint32_t, seed_hi) S(uint32_t, env_off_lo) S(uint32_t, env_off_hi)               \
     S(int32_t, env0)     /* first arena of this step launch (env groups on separate streams, swarm_capi.cpp) */ \
     S(int32_t, env_n)    /* arenas of this step launch (0 = all E) */                                        \
-    /* arena order (SWARM_ARENA_ORDER, swarm_step_impl.h): buffer address (0 = identity order), the     */   \
-    /* set read by this launch (0-2), its tag, and the cost classes (wave life in 1024-clock units)     */   \
-    S(uint32_t, order_lo) S(uint32_t, order_hi) S(int32_t, order_set) S(int32_t, order_tag)                 \
-    S(int32_t, order_c0) S(int32_t, order_cw)                                                               \
     /* ---- mission constants (compile time in the kernels) ---- */                                          \
     S(int32_t, nseg) S(int32_t, nint) /* raycast segments (arena 12 + internal), internal walls */           \
     S(int32_t, has_light)                                                                                   \
@@ -55,7 +45,6 @@ enum RngPurpose : uint32_t {
     S(float, wall_clear_dg) /* r + 0.5*t + eps (DG:1050-1054) */                                             \
     /* kernel pre-filters only: face offsets -(p.n), radii inside which no face is within reach */            \
     A(float, face_d, 12) S(float, wall_safe_r2) S(float, ins_safe_r2)                                       \
-    S(float, wall_mask_r2) /* |p|^2 below it: no face within clearance + SWARM_WALL_MARGIN (step kernel) */    \
     S(float, wall_clear_mc) /* r (MC:533) */                                                                 \
     /* internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 */                                      \
     A(float, iw_nx, 3) A(float, iw_ny, 3) A(float, iw_ax, 3) A(float, iw_ay, 3) A(float, iw_tx, 3)          \
@@ -77,25 +66,11 @@ enum RngPurpose : uint32_t {
     /* scalar constants; squared pre-filters: s >= x2_hi guarantees fl(sqrt(s)) >= x */                     \
     S(float, r_robot) S(float, min_dist) S(float, r2) S(float, max_speed) S(float, wheelbase) S(float, dt)  \
     S(float, min_dist2_hi) S(float, rab_range2_hi) S(float, inv_prox_range) S(float, inv_unity)             \
+    /* exact squared thresholds: fl(sqrt(s)) < R  <=>  s < x_s_lim (smallest float whose sqrt reaches R) */  \
+    S(float, min_dist_s_lim) S(float, rab_s_lim)                                                            \
     S(float, prox_range) S(float, rab_range) S(float, rab_loss) S(float, unity) S(float, light_thr)         \
     S(float, light_int) S(float, alpha) S(float, prox_thr) S(float, pi_f) S(float, two_pi_f)                \
     S(float, half_pi_f) S(float, critic_radius)
-
-// arena-order buffer of one handle (swarm_step_impl.h order_arena): 3 sets of kOrderHdr header
-// words + kOrderClasses bitmaps of order_wpc(E) words (padded so that each of the 64 lanes of
-// a wave reads a multiple of 4 words), then order_buffer_words - 3 sets = one float per arena
-constexpr int kOrderClasses = 8;
-constexpr int kOrderHdr = 16;
-constexpr int kOrderMaxEnvs = 16384;   // larger launches keep the identity order (scan cost)
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-constexpr int order_wpc(int E) { return ((((E + 31) >> 5) + 31) >> 5) << 5; }
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-constexpr size_t order_set_words(int E) { return (size_t)kOrderHdr + (size_t)kOrderClasses * (size_t)order_wpc(E); }
-constexpr size_t order_buffer_words(int E) { return 3 * order_set_words(E) + (size_t)E; }
 
 struct Geom {
 #define SWARM_GEOM_S(t, n) t n;

@@ -16,6 +16,15 @@ namespace swarm {
 
 constexpr double kPi = 3.14159265358979323846;
 
+// The smallest float s >= 0 whose correctly rounded float sqrt is >= R: fl(sqrt(s)) is
+// monotone, so fl(sqrt(s)) < R exactly when s < sqrt_lim(R) (std::sqrt(float) is IEEE).
+inline float sqrt_lim(float R) {
+    float s = R * R;
+    while (s > 0.0f && std::sqrt(s) >= R) s = std::nextafter(s, 0.0f);
+    while (std::sqrt(s) < R) s = std::nextafter(s, INFINITY);
+    return s;
+}
+
 inline void build_geom(const swarm_params_t& p, Geom& g) {
     std::memset(&g, 0, sizeof(g));
     const bool mc = p.profile == SWARM_PROFILE_STANDALONE;
@@ -79,8 +88,6 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     }
     const double rs = apo - g.wall_clear_dg - 1e-4, ri = apo - 1e-3 - 1e-4;
     g.wall_safe_r2 = (float)(rs * rs);
-    const double rm = rs - (double)SWARM_WALL_MARGIN;
-    g.wall_mask_r2 = (float)(rm * rm);
     g.ins_safe_r2 = (float)(ri * ri);
 
     // mission zones (DG:649-656, DGC:163-167; SH:24-27 / MC:322-329)
@@ -209,6 +216,8 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     // float pre-filter a strict superset of the exact test (the kernels re-check).
     g.min_dist2_hi = (float)((double)g.min_dist * g.min_dist * (1.0 + 1.0 / 1048576.0));
     g.rab_range2_hi = (float)((double)g.rab_range * g.rab_range * (1.0 + 1.0 / 1048576.0));
+    g.min_dist_s_lim = sqrt_lim(g.min_dist);
+    g.rab_s_lim = sqrt_lim(g.rab_range);
     g.inv_prox_range = 1.0f / g.prox_range;
     g.inv_unity = 1.0f / g.unity;
 }

@@ -117,15 +117,6 @@
 #define SWARM_RAY_PREFILTER 0
 #endif
 
-// 1: the arena-wall pushes of one solver call test only the faces some robot of the wave was
-// within clearance + SWARM_WALL_MARGIN of when the call began (one wave-uniform face mask,
-// rebuilt if any robot has since moved farther than the margin): a face outside it is farther
-// than the clearance from every robot, i.e. it would add pen = 0 (a +-0 term). The faces are
-// then walked with scalar bit tests instead of a vector test + branch per face per call.
-// Bitwise-neutral.
-#ifndef SWARM_WALL_MASK
-#define SWARM_WALL_MASK 0
-#endif
 
 // 1: the contact solver's pair term from one hardware reciprocal square root
 // (dist = s * rsq(s), the normal d * rsq(s)) instead of a correctly rounded sqrt
@@ -135,23 +126,25 @@
 #define SWARM_PAIR_RSQ 0
 #endif
 
-// 1: the contact solver's candidate loop takes a lane's candidates two at a time (the second
-// one's term computed as an independent chain and added, in increasing j, only if present), so
-// a lane with k candidates loops ceil(k / 2) times instead of k. Same terms in the same order:
-// bitwise-neutral.
-#ifndef SWARM_PAIR2
-#define SWARM_PAIR2 0
+// 1: the proximity pass's near-face test of a part covers only that part's arena faces
+// (s = p, p + 3, p + 6, p + 9), reading their (normal, offset) from a per-workgroup LDS table
+// instead of testing all 12 compile-time faces on every lane and masking 8 of them off. Same
+// expression per face: bitwise-neutral. Layout 103 only.
+#ifndef SWARM_FACE_SPLIT
+#define SWARM_FACE_SPLIT 0
 #endif
 
-// 1: arenas are handed to the workgroups of a layout-103 launch heaviest first. Each wave of a
-// launch files its arena under a cost class (its own life in shader clocks) in an order buffer
-// owned by the handle; the next launch gives block b the b-th arena of that order, so the
-// arenas that set the launch's length start first, one per SIMD, as the oldest wave there
-// (VALU issue goes by priority, then age). Scheduling only: every arena's arithmetic is the
-// same, so results are bitwise unchanged. See order_arena() for the set rotation and checks.
-#ifndef SWARM_ARENA_ORDER
-#define SWARM_ARENA_ORDER 0
+// 1: range-and-bearing terms without the correctly rounded distance: the in-range test is
+// exact on the squared distance (s < rab_s_lim, the smallest float whose sqrt reaches the range:
+// the same neighbours as fl(sqrt(s)) < range), so the candidate mask of the observation pass
+// IS the range test; the distance that only weights the bearing terms is s * rsq(s) and the
+// bearing's normaliser rsq(|b|^2) (~1-2 ulp: within the 1e-5 contract, NOT bitwise); the
+// line-of-sight test, whose outcome is discrete, keeps the correctly rounded distance.
+#ifndef SWARM_RAB_FAST
+#define SWARM_RAB_FAST 0
 #endif
+
+
 
 namespace swarm {
 
@@ -363,6 +356,9 @@ struct Shared {
 #if SWARM_ZT_TABLE
     float zt[64];       // ztilde of a range-and-bearing count
 #endif
+#if SWARM_FACE_SPLIT
+    float4 face[12];    // arena faces: normal (x, y), offset -(p . n), 0
+#endif
 };
 
 #if SWARM_SEG_LDS
@@ -382,6 +378,9 @@ __device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
 #endif
 #if SWARM_ZT_TABLE
     if (t < 64) S.zt[t] = 1.0f - 2.0f / (1.0f + expf((float)t));   // rab_finish's expression
+#endif
+#if SWARM_FACE_SPLIT
+    if (t < 12) S.face[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_d[t], 0.0f);
 #endif
     (void)g;
     (void)S;
@@ -454,7 +453,11 @@ __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const fl
         const float dx = p[jj].x - x, dy = p[jj].y - y;
         const float s = dx * dx + dy * dy;
         a |= (ok & (s <= 0.0200f)) ? (1u << jj) : 0u;
+#if SWARM_RAB_FAST
+        b |= (ok & (s + 1e-8f < g.rab_s_lim)) ? (1u << jj) : 0u;
+#else
         b |= (ok & (s + 1e-8f < g.rab_range2_hi)) ? (1u << jj) : 0u;
+#endif
     }
     mprox = a;
     mrab = b;
@@ -504,53 +507,6 @@ __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
         ty += pen * g.face_ny[k];
     }
 #endif
-    x = x + tx;
-    y = y + ty;
-}
-
-// Wave-uniform mask of the arena faces a walls_dg call may need (SWARM_WALL_MASK): face k is in
-// it if some robot's fused signed-distance estimate was below clearance + 1e-4 + margin at
-// (x0, y0); while no robot has moved margin away from (x0, y0) since, a face outside the mask
-// still has sd >= clearance + 1e-4 for every robot (|n_k| = 1), i.e. walls_dg's own per-face
-// filter would skip it.
-struct WallMask {
-    uint32_t faces;   // wave-uniform
-    float x0, y0;
-};
-
-__device__ __forceinline__ void wall_mask_build(const Geom& g, WallMask& w, float x, float y) {
-    uint32_t m = 0;
-    if (__any(fmaf(x, x, y * y) >= g.wall_mask_r2)) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const float sda = fmaf(x, g.face_nx[k], fmaf(y, g.face_ny[k], g.face_d[k]));
-            if (__any(sda < g.wall_clear_dg + 1e-4f + SWARM_WALL_MARGIN)) m |= 1u << k;
-        }
-    }
-    w.faces = m;
-    w.x0 = x;
-    w.y0 = y;
-}
-
-// walls_dg (DG:1048-1078) over the faces of a WallMask: the same terms in the same face order
-// (the skipped faces would add +-0); rebuilds the mask first if a robot left its margin
-__device__ __forceinline__ void walls_dg_masked(const Geom& g, WallMask& w, float& x, float& y) {
-    if (SWARM_ABLATE & 8) return;
-    const float dx = x - w.x0, dy = y - w.y0;
-    constexpr float lim = 0.999f * SWARM_WALL_MARGIN;
-    if (__any(dx * dx + dy * dy >= lim * lim)) wall_mask_build(g, w, x, y);
-    const uint32_t m = __builtin_amdgcn_readfirstlane(w.faces);
-    if (!m) return;   // no face within reach: every term is +-0 and x + 0 = x
-    float tx = 0.0f, ty = 0.0f;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        if (m & (1u << k)) {
-            const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
-            const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
-            tx += pen * g.face_nx[k];
-            ty += pen * g.face_ny[k];
-        }
-    }
     x = x + tx;
     y = y + ty;
 }
@@ -609,61 +565,16 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         cx += row ? 0.0f : -hx;
         cy += row ? 0.0f : -hy;
     };
-    // pair_term's half-overlap push (hx, hy) of one pair without the branch: (+0, +0) when the
-    // pair does not overlap, which leaves the sums it is added to unchanged
-    auto pair_push = [&](int, float dx, float dy, float& hx, float& hy) {
-#if SWARM_PAIR_RSQ
-        const float s2 = fmaf(dx, dx, fmaf(dy, dy, 1e-8f));
-        const float rs = __builtin_amdgcn_rsqf(s2);
-        const float ov = fmaf(-s2, rs, g.min_dist);
-        const float hh = ov > 0.0f ? ov * rs * 0.5f : 0.0f;
-        hx = hh * dx;
-        hy = hh * dy;
-#else
-        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
-        const float ov = g.min_dist - dist;
-        const float inv = frcp(dist + 1e-8f);
-        const bool on = ov > 0.0f;
-        hx = on ? ov * (dx * inv) * 0.5f : 0.0f;
-        hy = on ? ov * (dy * inv) * 0.5f : 0.0f;
-#endif
-    };
-    (void)pair_push;
     if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
         const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
             return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
         });
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
-#if SWARM_PAIR2
-        uint32_t cm = cand;
-        while (cm) {
-            SWARM_WT(L.wt_pair++);
-            const int j1 = L.j0 + __builtin_ctz(cm);
-            cm &= cm - 1u;
-            const bool two = cm != 0u;
-            const int j2 = two ? L.j0 + __builtin_ctz(cm) : j1;
-            cm &= two ? cm - 1u : cm;
-            const float2 p1 = S.xy[L.ab + j1], p2 = S.xy[L.ab + j2];
-            float h1x, h1y, h2x, h2y;
-            pair_push(j1, x - p1.x, y - p1.y, h1x, h1y);
-            pair_push(j2, x - p2.x, y - p2.y, h2x, h2y);
-            const bool r1 = j1 > L.i, r2 = j2 > L.i;
-            rx += r1 ? h1x : 0.0f;
-            ry += r1 ? h1y : 0.0f;
-            cx += r1 ? 0.0f : -h1x;
-            cy += r1 ? 0.0f : -h1y;
-            rx += (two & r2) ? h2x : 0.0f;
-            ry += (two & r2) ? h2y : 0.0f;
-            cx += (two & !r2) ? -h2x : 0.0f;
-            cy += (two & !r2) ? -h2y : 0.0f;
-        }
-#else
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
             pair_term(j, x - p.x, y - p.y);
         });
-#endif
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
     } else {
         unsigned long long cand = 0;
@@ -841,14 +752,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     constexpr bool apply = APPLY;
-#if SWARM_WALL_MASK
-    WallMask wmask;
-    wall_mask_build(g, wmask, x, y);
-#define SOLVE_WALLS(g, x, y) walls_dg_masked(g, wmask, x, y)
-#else
-#define SOLVE_WALLS(g, x, y) walls_dg(g, x, y)
-#endif
-    SOLVE_WALLS(g, x, y);
+    walls_dg(g, x, y);
     if constexpr (INTERNAL) {
         if (!apply) capsules(g, x, y, false, 0.0f, 0.0f);
     }
@@ -861,7 +765,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
         const float bx = x, by = y;
         bool pushed = false;
         if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
-        SOLVE_WALLS(g, x, y);
+        walls_dg(g, x, y);
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
             if (edge && !apply) {
@@ -955,10 +859,23 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         for (int s = 0; s < 32; s += ly_parts(LY)) m |= 1u << s;
         return m;
     }();
+#if SWARM_FACE_SPLIT
+    if constexpr (ly_parts(LY) == 3 && ly_waves(LY) == 1) {
 #pragma unroll
-    for (int s = 0; s < 12; ++s) {
-        const float sda = fmaf(x, g.face_nx[s], fmaf(y, g.face_ny[s], g.face_d[s]));
-        near_mask |= sda < g.prox_range + 1e-3f + 1e-4f ? (1u << s) : 0u;
+        for (int m = 0; m < 4; ++m) {
+            const int s = L.p + 3 * m;
+            const float4 f = S.face[s];
+            const float sda = fmaf(x, f.x, fmaf(y, f.y, f.z));
+            near_mask |= sda < g.prox_range + 1e-3f + 1e-4f ? (1u << s) : 0u;
+        }
+    } else
+#endif
+    {
+#pragma unroll
+        for (int s = 0; s < 12; ++s) {
+            const float sda = fmaf(x, g.face_nx[s], fmaf(y, g.face_ny[s], g.face_d[s]));
+            near_mask |= sda < g.prox_range + 1e-3f + 1e-4f ? (1u << s) : 0u;
+        }
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -1132,12 +1049,20 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
     ayy = 0.0f;
     // one kept, in-range neighbour (exact distance test, LOS, bearing terms)
     auto term = [&](int j, float dx, float dy) {
-        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
-        if (!(dist < g.rab_range)) return;
         // line of sight (ES:462-501): arena faces can only block if an end point is
         // not strictly inside the convex arena; internal walls are always tested.
         const bool test_arena = !(me_in && insv[L.ab + j] != 0);
         const int s0 = test_arena ? 0 : 12;
+#if SWARM_RAB_FAST
+        // pre_cand is the exact range test (obs_masks); without it (rab_only) test here
+        const float s2 = dx * dx + dy * dy + 1e-8f;
+        if (!pre_cand && !(s2 < g.rab_s_lim)) return;
+        float dist = s2 * __builtin_amdgcn_rsqf(s2);
+        if (s0 < g.nseg) dist = nsqrt(s2);
+#else
+        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
+        if (!(dist < g.rab_range)) return;
+#endif
         bool blocked = false;
         // no segment to test (convex arena only, both ends strictly inside): skip the divisions
         if (s0 < g.nseg) {
@@ -1169,7 +1094,11 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         const float hb2 = bx * bx + by * by;
         float cb = 1.0f, sb = 0.0f;
         if (hb2 > 0.0f) {
+#if SWARM_RAB_FAST
+            const float ih = __builtin_amdgcn_rsqf(hb2);
+#else
             const float ih = frcp(fsqrt(hb2));
+#endif
             cb = bx * ih;
             sb = by * ih;
         }
@@ -1666,89 +1595,6 @@ __device__ __forceinline__ float team_reward(const Geom& g, const Lane& L, float
 // ---------------------------------------------------------------------------
 //  The fused step kernel
 // ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-//  Arena order (SWARM_ARENA_ORDER). Buffer (swarm_geom.h order_set_words): 3 sets of
-//  kOrderHdr header words + kOrderClasses bitmaps of order_wpc(E) words (class slot 0 =
-//  heaviest), then one float per arena (its smoothed life). Launch t reads set R = order_set,
-//  files into W = R + 1 and clears X = R + 2 (mod 3): a set is cleared, filled by one launch
-//  and read by the next. Each wave of launch t sets its arena's bit in the bitmap of its cost
-//  class (one non-returning atomicOr); block b of launch t + 1 takes the b-th set bit in slot
-//  order. Header: [8] env0, [9] arenas of the writing launch, [10] its tag. A set is used only
-//  if its header matches this launch (env0, arena count, writer tag = reader tag - 1) and its
-//  bitmaps hold exactly as many bits as this launch has arenas (each filing wave sets one bit
-//  of its own arena, so the set is then a permutation; a set filed twice without a clear, as a
-//  graph replay of captured launches can do, either still is one or holds too many bits);
-//  otherwise block b takes arena b.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t* order_buf(const Geom& gr) {
-    return reinterpret_cast<uint32_t*>(((uint64_t)gr.order_hi << 32) | gr.order_lo);
-}
-
-// local arena (0 .. nblk-1) of block b
-__device__ __forceinline__ int order_arena(const Geom& gr, int nblk, int b) {
-    const int wpc = order_wpc(gr.E);
-    const uint32_t* h = order_buf(gr) + (size_t)gr.order_set * order_set_words(gr.E);
-    const bool hdr_ok = (int)__builtin_amdgcn_readfirstlane(h[8]) == gr.env0 &&
-                        (int)__builtin_amdgcn_readfirstlane(h[9]) == nblk &&
-                        (int)__builtin_amdgcn_readfirstlane(h[10]) == gr.order_tag - 1;
-    if (!hdr_ok) return b;
-    const int lane = threadIdx.x & 63;
-    const int per = wpc * kOrderClasses / 64;           // words per lane, a multiple of 4
-    const uint32_t* mine = h + kOrderHdr + (size_t)lane * per;
-    int cnt = 0;
-    for (int k = 0; k < per; k += 4) {
-        const uint4 v = *reinterpret_cast<const uint4*>(mine + k);
-        cnt += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-    }
-    int incl = cnt;   // inclusive prefix over the lanes
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(incl, d);
-        incl += lane >= d ? t : 0;
-    }
-    if (__builtin_amdgcn_readlane(incl, 63) != nblk) return b;
-    const int L = __ffsll((long long)__ballot(incl > b)) - 1;    // the lane holding set bit number b
-    int found = -1;
-    if (lane == L) {
-        int off = b - (incl - cnt);
-        for (int k = 0; k < per; ++k) {
-            uint32_t v = mine[k];
-            const int pc = __popc(v);
-            if (off < pc) {
-                for (; off > 0; --off) v &= v - 1u;
-                found = ((lane * per + k) % wpc) * 32 + __builtin_ctz(v);
-                break;
-            }
-            off -= pc;
-        }
-    }
-    found = __builtin_amdgcn_readlane(found, L);
-    return (found >= 0 && found < nblk) ? found : b;
-}
-
-// file this wave's arena under the class of its smoothed life (1024-clock units) for the next
-// launch; block 0 also writes W's header and clears X
-__device__ __forceinline__ void order_file(const Geom& gr, int nblk, int arena, float ema) {
-    uint32_t* base = order_buf(gr);
-    const size_t sw = order_set_words(gr.E);
-    const int wpc = order_wpc(gr.E);
-    uint32_t* w = base + (size_t)((gr.order_set + 1) % 3) * sw;
-    uint32_t* x = base + (size_t)((gr.order_set + 2) % 3) * sw;
-    const int k = (int)ema - gr.order_c0;
-    const int c = k < 0 ? 0 : min(kOrderClasses - 1, k / max(1, gr.order_cw));
-    if (threadIdx.x == 0) {
-        atomicOr(&w[kOrderHdr + (size_t)(kOrderClasses - 1 - c) * wpc + (arena >> 5)], 1u << (arena & 31));
-        reinterpret_cast<float*>(base + 3 * sw)[arena] = ema;
-        if (blockIdx.x == 0) {
-            w[8] = (uint32_t)gr.env0;
-            w[9] = (uint32_t)nblk;
-            w[10] = (uint32_t)gr.order_tag;
-        }
-    }
-    if (blockIdx.x == 0)
-        for (size_t i = threadIdx.x; i < sw; i += 64) x[i] = 0u;
-}
-
 // NA > 0: kernel specialised for NA robots per arena (the reference's 20), so
 // every neighbour loop has a compile-time trip count and is fully unrolled.
 template <int NA, int LY>
@@ -1822,19 +1668,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     const Geom& g = kGeomTab[MISSION][PROFILE];   // mission constants as literals; gr: runtime fields
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
-    int blk = (int)blockIdx.x;
-#if SWARM_ARENA_ORDER
-    constexpr bool ORDERED = !REPLAY && LY == 103;
-    const int nblk = gr.env_n > 0 ? gr.env_n : gr.E;
-    const bool ordered = ORDERED && (gr.order_lo | gr.order_hi) != 0;
-    const uint64_t ord_t0 = __builtin_amdgcn_s_memtime();
-    float ord_ema = 0.0f;
-    if (ordered) {
-        blk = order_arena(gr, nblk, blk);
-        ord_ema = reinterpret_cast<const float*>(order_buf(gr) + 3 * order_set_words(gr.E))[blk];
-    }
-#endif
-    const Lane L = make_lane<NA, LY>(gr, blk);
+    const Lane L = make_lane<NA, LY>(gr, (int)blockIdx.x);
     stage_tables<LY>(g, S);
     // 32-bit element indices (swarm_create bounds E*N*24 < 2^31) -> SGPR base + VGPR offset addressing
     const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
@@ -2016,12 +1850,6 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
         }
     }
-#if SWARM_ARENA_ORDER
-    if (ordered) {
-        const float life = (float)((__builtin_amdgcn_s_memtime() - ord_t0) >> 10);
-        order_file(gr, nblk, blk, ord_ema > 0.0f ? 0.5f * (ord_ema + life) : life);
-    }
-#endif
 #if SWARM_WAVE_TIMING
     if constexpr (!REPLAY && ly_waves(LY) == 1) {
         const uint64_t wt_c1 = __builtin_amdgcn_s_memtime();

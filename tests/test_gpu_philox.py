@@ -257,51 +257,3 @@ def test_step_groups_bitwise(mission, discrete, obs_dim, gpu_device):
             for name, x, y in zip(("obs", "reward", "trunc"), a, b):
                 assert np.array_equal(x, y), f"groups={groups}: decision {k} {name} differs"
 
-
-@pytest.mark.parametrize("mission,discrete,obs_dim", [("homing", False, 24), ("foraging", True, 4)])
-def test_arena_order_bitwise(mission, discrete, obs_dim, gpu_device, monkeypatch):
-    """Arena order (SWARM_ARENA_ORDER kernels; SWARM_ORDER=0 turns the handle's order buffer
-    off): handing the arenas to the workgroups heaviest first changes no result bit, eager and
-    under HIP-graph replays of captured launches (whose order tags repeat), with staggered
-    time-outs and fused 5-step decisions."""
-    from SwarmACB_isaac.engine import SwarmEngine
-
-    E, seed = 1000, 4242
-    rng = np.random.default_rng(11)
-    acts = [torch.as_tensor(rng.integers(0, 6, (E, 20)).astype(np.int32) if discrete
-                            else (np.clip(rng.normal(size=(E, 20, 2)), -3, 3) / 3).astype(np.float32)).to(gpu_device)
-            for _ in range(14)]
-    runs = []
-    for order in ("0", "1"):
-        monkeypatch.setenv("SWARM_ORDER", order)
-        eng = SwarmEngine(mission, "isaac", E, 20, obs_dim, discrete, 1800, 1, 0, seed, gpu_device)
-        eng.reset()
-        _stagger_timeouts(eng, [(np.arange(3, 13), 3), (np.arange(400, 407), 17), ([E - 1], 31)])
-        outs = []
-        for k in range(8):
-            obs, rew, tr = eng.step(acts[k], 5)
-            outs.append((obs.clone(), rew.clone(), tr.clone()))
-        # two launches captured once, replayed three times
-        static = acts[8].clone()
-        stream = torch.cuda.Stream(gpu_device)
-        stream.wait_stream(torch.cuda.current_stream(gpu_device))
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(stream):
-            with torch.cuda.graph(g, stream=stream):
-                o1 = eng.step(static, 5)
-                o2 = eng.step(static, 5)
-        torch.cuda.current_stream(gpu_device).wait_stream(stream)
-        for k in range(3):
-            static.copy_(acts[9 + k])
-            g.replay()
-            outs.append(tuple(t.clone() for t in o1 + o2))
-        torch.cuda.synchronize(gpu_device)
-        runs.append((eng.dump_state(), [tuple(t.cpu().numpy() for t in o) for o in outs]))
-        del g
-        eng.close()
-    (ref_state, ref_outs), (st, outs) = runs
-    for key in ref_state:
-        assert np.array_equal(ref_state[key], st[key]), f"state {key} differs"
-    for k, (a, b) in enumerate(zip(ref_outs, outs)):
-        for j, (x, y) in enumerate(zip(a, b)):
-            assert np.array_equal(x, y), f"decision {k} output {j} differs"
