@@ -134,6 +134,15 @@
 #define SWARM_FACE_SPLIT 0
 #endif
 
+// 1: the arena-wall pushes of the contact solver (walls_dg, 7 calls per substep) split over the
+// 3 parts of a robot (layout 103): part p tests faces p, p + 3, p + 6, p + 9 (normals, offsets
+// and anchors from a per-workgroup LDS table) and the parts' pushes meet through LDS, only
+// when some lane was pushed. A robot touches at most two faces, which fall in different parts,
+// and IEEE addition is commutative, so the sum is the reference's face-order sum bit for bit.
+#ifndef SWARM_WALL_SPLIT
+#define SWARM_WALL_SPLIT 0
+#endif
+
 // 1: range-and-bearing terms without the correctly rounded distance: the in-range test is
 // exact on the squared distance (s < rab_s_lim, the smallest float whose sqrt reaches the range:
 // the same neighbours as fl(sqrt(s)) < range), so the candidate mask of the observation pass
@@ -356,8 +365,12 @@ struct Shared {
 #if SWARM_ZT_TABLE
     float zt[64];       // ztilde of a range-and-bearing count
 #endif
-#if SWARM_FACE_SPLIT
+#if SWARM_FACE_SPLIT || SWARM_WALL_SPLIT
     float4 face[12];    // arena faces: normal (x, y), offset -(p . n), 0
+#endif
+#if SWARM_WALL_SPLIT
+    float2 facep[12];   // arena faces: anchor point
+    float2 wred[64];    // the parts' wall pushes
 #endif
 };
 
@@ -379,8 +392,11 @@ __device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
 #if SWARM_ZT_TABLE
     if (t < 64) S.zt[t] = 1.0f - 2.0f / (1.0f + expf((float)t));   // rab_finish's expression
 #endif
-#if SWARM_FACE_SPLIT
+#if SWARM_FACE_SPLIT || SWARM_WALL_SPLIT
     if (t < 12) S.face[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_d[t], 0.0f);
+#endif
+#if SWARM_WALL_SPLIT
+    if (t < 12) S.facep[t] = make_float2(g.face_px[t], g.face_py[t]);
 #endif
     (void)g;
     (void)S;
@@ -510,6 +526,40 @@ __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
     x = x + tx;
     y = y + ty;
 }
+
+#if SWARM_WALL_SPLIT
+// walls_dg with the 12 faces split over the 3 parts of a robot (SWARM_WALL_SPLIT). The first
+// read of the face table follows publish()'s exchange point (ordered after stage_tables).
+template <int LY>
+__device__ __forceinline__ void walls_dg_split(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
+    if (SWARM_ABLATE & 8) return;
+    float tx = 0.0f, ty = 0.0f;
+    if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int k = L.p + 3 * m;
+            const float4 f = S.face[k];
+            const float sda = fmaf(x, f.x, fmaf(y, f.y, f.z));
+            if (__any(sda < g.wall_clear_dg + 1e-4f)) {
+                const float2 q = S.facep[k];
+                const float sd = (x - q.x) * f.x + (y - q.y) * f.y;
+                const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
+                tx += pen * f.x;
+                ty += pen * f.y;
+            }
+        }
+        if (__any(tx != 0.0f || ty != 0.0f)) {
+            S.wred[L.tid] = make_float2(tx, ty);
+            sync_wg<LY>();
+            const float2 a = S.wred[L.pbase], b = S.wred[L.pbase + 1], c = S.wred[L.pbase + 2];
+            tx = (a.x + b.x) + c.x;
+            ty = (a.y + b.y) + c.y;
+        }
+    }
+    x = x + tx;
+    y = y + ty;
+}
+#endif
 
 // MC:531-553 — sequential per face with the robot radius as clearance.
 __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
@@ -752,7 +802,17 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     constexpr bool apply = APPLY;
-    walls_dg(g, x, y);
+#if SWARM_WALL_SPLIT
+    constexpr bool WSPLIT = ly_parts(LY) == 3 && ly_waves(LY) == 1;
+#define SOLVE_WALLS()                                        \
+    do {                                                     \
+        if constexpr (WSPLIT) walls_dg_split<LY>(g, L, S, x, y); \
+        else walls_dg(g, x, y);                              \
+    } while (0)
+#else
+#define SOLVE_WALLS() walls_dg(g, x, y)
+#endif
+    SOLVE_WALLS();
     if constexpr (INTERNAL) {
         if (!apply) capsules(g, x, y, false, 0.0f, 0.0f);
     }
@@ -765,7 +825,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
         const float bx = x, by = y;
         bool pushed = false;
         if (it < K) pushed = robots_push<LY, C>(g, L, S, x, y);
-        walls_dg(g, x, y);
+        SOLVE_WALLS();
         if constexpr (INTERNAL) {
             const bool edge = apply ? (it == 0 || it == K) : (it == K);
             if (edge && !apply) {
@@ -800,6 +860,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
 #endif
         }
     }
+#undef SOLVE_WALLS
 }
 
 // ---------------------------------------------------------------------------
