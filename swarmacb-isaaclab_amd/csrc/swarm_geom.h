@@ -46,6 +46,9 @@ enum RngPurpose : uint32_t {
     /* kernel pre-filters only: face offsets -(p.n), radii inside which no face is within reach */            \
     A(float, face_d, 12) S(float, wall_safe_r2) S(float, ins_safe_r2)                                       \
     S(float, wall_clear_mc) /* r (MC:533) */                                                                 \
+    /* per 15-degree sector of a position's direction: the 3 faces whose normals are nearest the sector */   \
+    /* centre, ascending, 4 bits each (step kernel SWARM_WALL_NEAR)                                     */   \
+    A(int32_t, wall_sector3, 24)                                                                            \
     /* internal walls (DG:898-1046): normal, anchor, tangent, |t|^2 */                                      \
     A(float, iw_nx, 3) A(float, iw_ny, 3) A(float, iw_ax, 3) A(float, iw_ay, 3) A(float, iw_tx, 3)          \
     A(float, iw_ty, 3) A(float, iw_lsq, 3) S(float, iw_clear_tunnel) S(float, iw_clear_capsule)             \

@@ -88,6 +88,25 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     }
     const double rs = apo - g.wall_clear_dg - 1e-4, ri = apo - 1e-3 - 1e-4;
     g.wall_safe_r2 = (float)(rs * rs);
+    // the 3 faces whose midpoints' directions are nearest to the centre of each 15-degree sector of
+    // a position's direction, ascending (a position within the wall clearance of face k lies within
+    // 15 degrees + a little of that face's direction, hence within 27 degrees of the centre of its
+    // sector even with the kernel's ~4-degree angle estimate: among these 3)
+    for (int sct = 0; sct < 24; ++sct) {
+        const double c = (15.0 * sct + 7.5) * kPi / 180.0;
+        int best[12];
+        double dist[12];
+        for (int k = 0; k < 12; ++k) {
+            double a = std::atan2((double)g.face_py[k], (double)g.face_px[k]) - c;
+            while (a > kPi) a -= 2.0 * kPi;
+            while (a < -kPi) a += 2.0 * kPi;
+            dist[k] = std::fabs(a);
+            best[k] = k;
+        }
+        std::sort(best, best + 12, [&](int a, int b) { return dist[a] < dist[b] || (dist[a] == dist[b] && a < b); });
+        std::sort(best, best + 3);
+        g.wall_sector3[sct] = best[0] | (best[1] << 4) | (best[2] << 8);
+    }
     g.ins_safe_r2 = (float)(ri * ri);
 
     // mission zones (DG:649-656, DGC:163-167; SH:24-27 / MC:322-329)

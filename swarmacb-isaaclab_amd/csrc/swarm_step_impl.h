@@ -143,6 +143,24 @@
 #define SWARM_WALL_SPLIT 0
 #endif
 
+// 1: the squared neighbour distances of the candidate masks (contact solver, observation) and of
+// the contact pair term as packed-f32 operations on (x, y) pairs (v_pk_add_f32 / v_pk_mul_f32):
+// the same two roundings per component and the same final add, so bitwise-neutral; two VALU
+// instructions fewer per distance.
+#ifndef SWARM_PK_DIST
+#define SWARM_PK_DIST 0
+#endif
+
+// 1: each arena-wall push of the contact solver (walls_dg, 7 calls per substep) evaluates only
+// the 3 faces that can be within the clearance of the robot: those nearest its direction
+// (wall_sector3 of the 15-degree sector of an octant-folded angle estimate, chosen once per
+// solver call: the solver moves a robot by millimetres, the sector window has >3 degrees to
+// spare), read from an LDS face table, in ascending face order. Every other face is farther
+// than the clearance and would add pen = 0: bitwise-neutral. Instead of 12 faces per call.
+#ifndef SWARM_WALL_NEAR
+#define SWARM_WALL_NEAR 0
+#endif
+
 // 1: range-and-bearing terms without the correctly rounded distance: the in-range test is
 // exact on the squared distance (s < rab_s_lim, the smallest float whose sqrt reaches the range:
 // the same neighbours as fl(sqrt(s)) < range), so the candidate mask of the observation pass
@@ -372,6 +390,10 @@ struct Shared {
     float2 facep[12];   // arena faces: anchor point
     float2 wred[64];    // the parts' wall pushes
 #endif
+#if SWARM_WALL_NEAR
+    float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
+    int wsec[24];       // wall_sector3
+#endif
 };
 
 #if SWARM_SEG_LDS
@@ -379,6 +401,21 @@ struct Shared {
 #else
 #define SEG_LDS_PTR(S) ((const float4*)nullptr)
 #endif
+
+// Workgroup-wide exchange point of the LDS tile / partial slots. With one wave
+// per workgroup (layouts 1 and 103) the wave's LDS instructions execute in
+// program order, so a later read sees an earlier write without waiting for it:
+// only the compiler must keep the order (wave-scope fence + wave barrier, no
+// s_waitcnt / s_barrier). Multi-wave layouts need the real barrier.
+template <int LY>
+__device__ __forceinline__ void sync_wg() {
+    if constexpr (ly_waves(LY) == 1 && SWARM_WAVE_SYNC) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
 
 // Per-workgroup tables staged once per launch (SWARM_SEG_LDS, SWARM_ZT_TABLE). The first
 // read follows publish()'s exchange point, which orders it after these writes.
@@ -398,24 +435,16 @@ __device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
 #if SWARM_WALL_SPLIT
     if (t < 12) S.facep[t] = make_float2(g.face_px[t], g.face_py[t]);
 #endif
+#if SWARM_WALL_NEAR
+    if (t < 12) S.wface[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_px[t], g.face_py[t]);
+    if (t < 24) S.wsec[t] = g.wall_sector3[t];
+#endif
     (void)g;
     (void)S;
     (void)t;
-}
-
-// Workgroup-wide exchange point of the LDS tile / partial slots. With one wave
-// per workgroup (layouts 1 and 103) the wave's LDS instructions execute in
-// program order, so a later read sees an earlier write without waiting for it:
-// only the compiler must keep the order (wave-scope fence + wave barrier, no
-// s_waitcnt / s_barrier). Multi-wave layouts need the real barrier.
-template <int LY>
-__device__ __forceinline__ void sync_wg() {
-    if constexpr (ly_waves(LY) == 1 && SWARM_WAVE_SYNC) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    } else {
-        __syncthreads();
-    }
+#if SWARM_WALL_NEAR
+    sync_wg<LY>();   // the solver reads the wall tables before any other exchange point
+#endif
 }
 
 #if SWARM_PRIO_MODE == 2
@@ -433,12 +462,32 @@ __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     return __popcll(m & L.amask);
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// (a - b) per component and |a - b|^2 = dx * dx + dy * dy with the reference's roundings
+// (packed under SWARM_PK_DIST: one subtraction and one multiplication for both components)
+__device__ __forceinline__ float sq_dist(float ax, float ay, float bx, float by, float& dx, float& dy) {
+#if SWARM_PK_DIST
+    const f2v d = f2v{ax, ay} - f2v{bx, by};
+    const f2v q = d * d;
+    dx = d.x;
+    dy = d.y;
+    return q.x + q.y;
+#else
+    dx = ax - bx;
+    dy = ay - by;
+    return dx * dx + dy * dy;
+#endif
+}
+
 // Candidate bits of this part's neighbour chunk j0 + jj, jj < C (compile time):
 // bit jj set iff j0 + jj < j1, j0 + jj != i and pred(dx, dy) for d = p_j - p_i.
 // All C tile entries are read first (indices stay inside the 64-entry tile;
 // entries past j1 are read but masked), then tested without branches.
+// pred(dx, dy) with d = p_j - p_i, or (abs_pos) pred(p_j.x, p_j.y)
 template <int C, class Pred>
-__device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, float x, float y, Pred pred) {
+__device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, float x, float y, Pred pred,
+                                               bool abs_pos = false) {
     float2 p[C];
 #pragma unroll
     for (int jj = 0; jj < C; ++jj) p[jj] = xy[L.ab + L.j0 + jj];
@@ -446,7 +495,7 @@ __device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, 
 #pragma unroll
     for (int jj = 0; jj < C; ++jj) {
         const int j = L.j0 + jj;
-        const bool c = (j < L.j1) & (j != L.i) & pred(p[jj].x - x, p[jj].y - y);
+        const bool c = (j < L.j1) & (j != L.i) & (abs_pos ? pred(p[jj].x, p[jj].y) : pred(p[jj].x - x, p[jj].y - y));
         m |= c ? (1u << jj) : 0u;
     }
     return m;
@@ -466,8 +515,8 @@ __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const fl
     for (int jj = 0; jj < C; ++jj) {
         const int j = L.j0 + jj;
         const bool ok = (j < L.j1) & (j != L.i);
-        const float dx = p[jj].x - x, dy = p[jj].y - y;
-        const float s = dx * dx + dy * dy;
+        float dx, dy;
+        const float s = sq_dist(p[jj].x, p[jj].y, x, y, dx, dy);
         a |= (ok & (s <= 0.0200f)) ? (1u << jj) : 0u;
 #if SWARM_RAB_FAST
         b |= (ok & (s + 1e-8f < g.rab_s_lim)) ? (1u << jj) : 0u;
@@ -526,6 +575,43 @@ __device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
     x = x + tx;
     y = y + ty;
 }
+
+#if SWARM_WALL_NEAR
+// the packed 3 candidate faces of a position (wall_sector3 of its direction's 15-degree sector;
+// the angle estimate t * 45 degrees on the octant-folded ratio is within 4.1 degrees)
+template <int LY>
+__device__ __forceinline__ int wall_faces(const Shared<LY>& S, float x, float y) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mn = fminf(ax, ay), mx = fmaxf(ax, ay);
+    const float t = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
+    float a = t * 45.0f;
+    a = ay > ax ? 90.0f - a : a;
+    a = x < 0.0f ? 180.0f - a : a;
+    a = y < 0.0f ? 360.0f - a : a;
+    const int sct = min(23, max(0, (int)(a * (1.0f / 15.0f))));
+    return S.wsec[sct];
+}
+
+// walls_dg (DG:1048-1078) over the 3 packed candidate faces, ascending: the other faces add
+// pen = 0, and the sum of the rest is in the reference's face order
+template <int LY>
+__device__ __forceinline__ void walls_dg_near(const Geom& g, const Shared<LY>& S, int faces, float& x, float& y) {
+    if (SWARM_ABLATE & 8) return;
+    float tx = 0.0f, ty = 0.0f;
+    if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            const float4 f = S.wface[(faces >> (4 * m)) & 15];
+            const float sd = (x - f.z) * f.x + (y - f.w) * f.y;
+            const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
+            tx += pen * f.x;
+            ty += pen * f.y;
+        }
+    }
+    x = x + tx;
+    y = y + ty;
+}
+#endif
 
 #if SWARM_WALL_SPLIT
 // walls_dg with the 12 faces split over the 3 parts of a robot (SWARM_WALL_SPLIT). The first
@@ -589,7 +675,10 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
     // candidate pairs from the squared distance (a superset: s >= md2_hi implies
     // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
-    auto pair_term = [&](int j, float dx, float dy) {
+    auto pair_term = [&](int j, float2 pj) {
+        float dx, dy;
+        const float dd2 = sq_dist(x, y, pj.x, pj.y, dx, dy);
+        (void)dd2;
 #if SWARM_PAIR_RSQ
         const float s2 = fmaf(dx, dx, fmaf(dy, dy, 1e-8f));
         const float rs = __builtin_amdgcn_rsqf(s2);
@@ -598,7 +687,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         const float hh = ov * rs * 0.5f;
         const float hx = hh * dx, hy = hh * dy;
 #else
-        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
+        const float dist = nsqrt(dd2 + 1e-8f);
         const float ov = g.min_dist - dist;
         if (!(ov > 0.0f)) return;
         const float inv = frcp(dist + 1e-8f);
@@ -617,13 +706,14 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     };
     if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
-        const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float dx, float dy) {
-            return dx * dx + dy * dy + 1e-8f < g.min_dist2_hi;
-        });
+        const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float px, float py) {
+            float dx, dy;
+            return sq_dist(px, py, x, y, dx, dy) + 1e-8f < g.min_dist2_hi;
+        }, true);
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
-            pair_term(j, x - p.x, y - p.y);
+            pair_term(j, p);
         });
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
     } else {
@@ -640,8 +730,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         while (cand) {
             const int j = __builtin_ctzll(cand);
             cand &= cand - 1ull;
-            const float2 p = S.xy[L.ab + j];
-            pair_term(j, x - p.x, y - p.y);
+            pair_term(j, S.xy[L.ab + j]);
         }
     }
     if constexpr (ly_parts(LY) > 1) {
@@ -802,7 +891,10 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     constexpr bool apply = APPLY;
-#if SWARM_WALL_SPLIT
+#if SWARM_WALL_NEAR
+    const int wfaces = wall_faces<LY>(S, x, y);
+#define SOLVE_WALLS() walls_dg_near<LY>(g, S, wfaces, x, y)
+#elif SWARM_WALL_SPLIT
     constexpr bool WSPLIT = ly_parts(LY) == 3 && ly_waves(LY) == 1;
 #define SOLVE_WALLS()                                        \
     do {                                                     \
