@@ -86,92 +86,24 @@
 #define SWARM_CR_SQRT 1
 #endif
 
-// 1: the raycast segment table (anchor, direction) is staged once per workgroup in
-// LDS; the proximity rays and the line-of-sight test read a segment with one
-// ds_read_b128 instead of four global loads of the constant table (a per-lane
-// segment index cannot use scalar loads). Same values: bitwise-neutral.
-#ifndef SWARM_SEG_LDS
-#define SWARM_SEG_LDS 0
-#endif
-
-// 1: ztilde = 1 - 2 / (1 + exp(n)) of the range-and-bearing count n (an integer,
-// ES:452) from a per-workgroup LDS table filled once per launch with the same
-// expression: one ds_read per substep instead of expf + an IEEE division. Bitwise-neutral.
-#ifndef SWARM_ZT_TABLE
-#define SWARM_ZT_TABLE 0
-#endif
-
-// 1: in the continuous-action Isaac profile the sensor-cache aggregates (the proximity
-// and light vector sums' magnitude / angle: sqrt + atan2) are evaluated only in the
-// last substep of a launch: nothing reads them in between (the behaviour modules are
-// discrete-only) and the cache is stored once per launch. Bitwise-neutral.
-#ifndef SWARM_LAST_CACHE
-#define SWARM_LAST_CACHE 0
-#endif
-
-// 1: the proximity rays of a near wall segment are pre-tested wave-uniformly with a
-// superset of the hit test (the ray points at the segment's line, t in [0, range] from
-// the signs and magnitudes of the two cross products, no reciprocal): a ray no active
-// lane can hit is skipped (it would leave every reading unchanged). Bitwise-neutral.
-#ifndef SWARM_RAY_PREFILTER
-#define SWARM_RAY_PREFILTER 0
-#endif
-
-
-// 1: the contact solver's pair term from one hardware reciprocal square root
-// (dist = s * rsq(s), the normal d * rsq(s)) instead of a correctly rounded sqrt
-// and a reciprocal of dist + 1e-8: the same formula within ~2 ulp of dist, i.e.
-// ~1e-8 m per pair push, far inside the 1e-5 teacher-forced contract (NOT bitwise).
-#ifndef SWARM_PAIR_RSQ
-#define SWARM_PAIR_RSQ 0
-#endif
-
-// 1: the proximity pass's near-face test of a part covers only that part's arena faces
-// (s = p, p + 3, p + 6, p + 9), reading their (normal, offset) from a per-workgroup LDS table
-// instead of testing all 12 compile-time faces on every lane and masking 8 of them off. Same
-// expression per face: bitwise-neutral. Layout 103 only.
-#ifndef SWARM_FACE_SPLIT
-#define SWARM_FACE_SPLIT 0
-#endif
-
-// 1: the arena-wall pushes of the contact solver (walls_dg, 7 calls per substep) split over the
-// 3 parts of a robot (layout 103): part p tests faces p, p + 3, p + 6, p + 9 (normals, offsets
-// and anchors from a per-workgroup LDS table) and the parts' pushes meet through LDS, only
-// when some lane was pushed. A robot touches at most two faces, which fall in different parts,
-// and IEEE addition is commutative, so the sum is the reference's face-order sum bit for bit.
-#ifndef SWARM_WALL_SPLIT
-#define SWARM_WALL_SPLIT 0
-#endif
-
-// 1: the squared neighbour distances of the candidate masks (contact solver, observation) and of
-// the contact pair term as packed-f32 operations on (x, y) pairs (v_pk_add_f32 / v_pk_mul_f32):
-// the same two roundings per component and the same final add, so bitwise-neutral; two VALU
-// instructions fewer per distance.
-#ifndef SWARM_PK_DIST
-#define SWARM_PK_DIST 0
-#endif
-
-// 1: each arena-wall push of the contact solver (walls_dg, 7 calls per substep) evaluates only
-// the 3 faces that can be within the clearance of the robot: those nearest its direction
-// (wall_sector3 of the 15-degree sector of an octant-folded angle estimate, chosen once per
-// solver call: the solver moves a robot by millimetres, the sector window has >3 degrees to
-// spare), read from an LDS face table, in ascending face order. Every other face is farther
-// than the clearance and would add pen = 0: bitwise-neutral. Instead of 12 faces per call.
-#ifndef SWARM_WALL_NEAR
-#define SWARM_WALL_NEAR 0
-#endif
-
-// 1: range-and-bearing terms without the correctly rounded distance: the in-range test is
-// exact on the squared distance (s < rab_s_lim, the smallest float whose sqrt reaches the range:
-// the same neighbours as fl(sqrt(s)) < range), so the candidate mask of the observation pass
-// IS the range test; the distance that only weights the bearing terms is s * rsq(s) and the
-// bearing's normaliser rsq(|b|^2) (~1-2 ulp: within the 1e-5 contract, NOT bitwise); the
-// line-of-sight test, whose outcome is discrete, keeps the correctly rounded distance.
-#ifndef SWARM_RAB_FAST
-#define SWARM_RAB_FAST 0
-#endif
-
-
+// Arithmetic shortcuts of the product kernel, all inside the parity contract (DESIGN.md §4,
+// round 4; the measured alternatives are recorded in profiles/r04/step/):
+//  * arena-wall pushes (walls_dg_near, 7 calls per substep) evaluate only the 3 faces nearest a
+//    robot's direction (wall_sector3 of the 15-degree sector of an octant-folded angle estimate,
+//    chosen once per solver call), read from an LDS face table in ascending face order; every
+//    other face is farther than the clearance and would add pen = 0: bitwise-neutral;
+//  * the proximity pass's near-face test of a part covers only that part's faces (s = p, p + 3,
+//    p + 6, p + 9) from the same LDS table: bitwise-neutral;
+//  * ztilde = 1 - 2 / (1 + exp(n)) of the integer range-and-bearing count n (ES:452) comes from a
+//    per-workgroup LDS table filled with the same expression: bitwise-neutral;
+//  * with continuous actions (Isaac profile) the sensor-cache aggregates (vector sums' magnitude /
+//    angle) are evaluated in the last substep of a launch only: nothing reads them in between;
+//  * range-and-bearing terms: the in-range test is exact on the squared distance (s < rab_s_lim,
+//    the smallest float whose correctly rounded sqrt reaches the range), so the observation
+//    pass's candidate mask IS the range test; the distance that only weights the bearing terms
+//    is s * rsq(s) and the bearing's normaliser rsq(|b|^2) (~1-2 ulp: NOT bitwise, within the
+//    1e-5 contract); the line-of-sight test, whose outcome is discrete, keeps the correctly
+//    rounded distance.
 
 namespace swarm {
 
@@ -377,30 +309,12 @@ struct Shared {
     float2 xy[64];
     int ins[64];
     float4 red[4][64 * ly_waves(LY)];
-#if SWARM_SEG_LDS
-    float4 seg[16];     // raycast segments: anchor (x, y), direction (x, y)
-#endif
-#if SWARM_ZT_TABLE
     float zt[64];       // ztilde of a range-and-bearing count
-#endif
-#if SWARM_FACE_SPLIT || SWARM_WALL_SPLIT
     float4 face[12];    // arena faces: normal (x, y), offset -(p . n), 0
-#endif
-#if SWARM_WALL_SPLIT
-    float2 facep[12];   // arena faces: anchor point
-    float2 wred[64];    // the parts' wall pushes
-#endif
-#if SWARM_WALL_NEAR
     float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
     int wsec[24];       // wall_sector3
-#endif
 };
 
-#if SWARM_SEG_LDS
-#define SEG_LDS_PTR(S) ((const float4*)(S).seg)
-#else
-#define SEG_LDS_PTR(S) ((const float4*)nullptr)
-#endif
 
 // Workgroup-wide exchange point of the LDS tile / partial slots. With one wave
 // per workgroup (layouts 1 and 103) the wave's LDS instructions execute in
@@ -417,34 +331,19 @@ __device__ __forceinline__ void sync_wg() {
     }
 }
 
-// Per-workgroup tables staged once per launch (SWARM_SEG_LDS, SWARM_ZT_TABLE). The first
+// Per-workgroup tables staged once per launch (ztilde, arena faces, wall sectors). The first
 // read follows publish()'s exchange point, which orders it after these writes.
 template <int LY>
 __device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
     const int t = threadIdx.x;
-#if SWARM_SEG_LDS
-    if (t < 16) S.seg[t] = t < g.nseg ? make_float4(g.seg_ax[t], g.seg_ay[t], g.seg_sx[t], g.seg_sy[t])
-                                      : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-#endif
-#if SWARM_ZT_TABLE
     if (t < 64) S.zt[t] = 1.0f - 2.0f / (1.0f + expf((float)t));   // rab_finish's expression
-#endif
-#if SWARM_FACE_SPLIT || SWARM_WALL_SPLIT
     if (t < 12) S.face[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_d[t], 0.0f);
-#endif
-#if SWARM_WALL_SPLIT
-    if (t < 12) S.facep[t] = make_float2(g.face_px[t], g.face_py[t]);
-#endif
-#if SWARM_WALL_NEAR
     if (t < 12) S.wface[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_px[t], g.face_py[t]);
     if (t < 24) S.wsec[t] = g.wall_sector3[t];
-#endif
     (void)g;
     (void)S;
     (void)t;
-#if SWARM_WALL_NEAR
     sync_wg<LY>();   // the solver reads the wall tables before any other exchange point
-#endif
 }
 
 #if SWARM_PRIO_MODE == 2
@@ -462,22 +361,11 @@ __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     return __popcll(m & L.amask);
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
 // (a - b) per component and |a - b|^2 = dx * dx + dy * dy with the reference's roundings
-// (packed under SWARM_PK_DIST: one subtraction and one multiplication for both components)
 __device__ __forceinline__ float sq_dist(float ax, float ay, float bx, float by, float& dx, float& dy) {
-#if SWARM_PK_DIST
-    const f2v d = f2v{ax, ay} - f2v{bx, by};
-    const f2v q = d * d;
-    dx = d.x;
-    dy = d.y;
-    return q.x + q.y;
-#else
     dx = ax - bx;
     dy = ay - by;
     return dx * dx + dy * dy;
-#endif
 }
 
 // Candidate bits of this part's neighbour chunk j0 + jj, jj < C (compile time):
@@ -518,11 +406,7 @@ __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const fl
         float dx, dy;
         const float s = sq_dist(p[jj].x, p[jj].y, x, y, dx, dy);
         a |= (ok & (s <= 0.0200f)) ? (1u << jj) : 0u;
-#if SWARM_RAB_FAST
         b |= (ok & (s + 1e-8f < g.rab_s_lim)) ? (1u << jj) : 0u;
-#else
-        b |= (ok & (s + 1e-8f < g.rab_range2_hi)) ? (1u << jj) : 0u;
-#endif
     }
     mprox = a;
     mrab = b;
@@ -542,41 +426,6 @@ __device__ __forceinline__ void for_each_cand(const Lane& L, const float2* xy, u
 //  Collisions
 // ---------------------------------------------------------------------------
 
-// DG:1048-1078 — inward push summed over all penetrated faces (Jacobi).
-// Wave-uniform pre-filters skip the faces no lane of the wave can reach: a face
-// whose exact signed distance exceeds the clearance contributes pen = 0, and a
-// +-0 term leaves the sum bitwise unchanged, so only the work changes. The
-// filters use a fused estimate of sd with a 1e-4 m margin (its error is ~1e-7).
-__device__ __forceinline__ void walls_dg(const Geom& g, float& x, float& y) {
-    if (SWARM_ABLATE & 8) return;
-    float tx = 0.0f, ty = 0.0f;
-#if SWARM_WALL_FILTER
-    if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const float sda = fmaf(x, g.face_nx[k], fmaf(y, g.face_ny[k], g.face_d[k]));
-            if (__any(sda < g.wall_clear_dg + 1e-4f)) {
-                const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
-                const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
-                tx += pen * g.face_nx[k];
-                ty += pen * g.face_ny[k];
-            }
-        }
-    }
-#else
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const float sd = (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k];
-        const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
-        tx += pen * g.face_nx[k];
-        ty += pen * g.face_ny[k];
-    }
-#endif
-    x = x + tx;
-    y = y + ty;
-}
-
-#if SWARM_WALL_NEAR
 // the packed 3 candidate faces of a position (wall_sector3 of its direction's 15-degree sector;
 // the angle estimate t * 45 degrees on the octant-folded ratio is within 4.1 degrees)
 template <int LY>
@@ -592,8 +441,11 @@ __device__ __forceinline__ int wall_faces(const Shared<LY>& S, float x, float y)
     return S.wsec[sct];
 }
 
-// walls_dg (DG:1048-1078) over the 3 packed candidate faces, ascending: the other faces add
-// pen = 0, and the sum of the rest is in the reference's face order
+// DG:1048-1078 — inward push summed over the penetrated faces (Jacobi), over the 3 packed
+// candidate faces in ascending order: every other face is farther than the clearance and would
+// add pen = 0 (a +-0 term leaves the sum bitwise unchanged), so the sum is the reference's
+// face-order sum. The wave skips the faces altogether when no robot is within the clearance of
+// the inscribed circle's rim.
 template <int LY>
 __device__ __forceinline__ void walls_dg_near(const Geom& g, const Shared<LY>& S, int faces, float& x, float& y) {
     if (SWARM_ABLATE & 8) return;
@@ -611,41 +463,7 @@ __device__ __forceinline__ void walls_dg_near(const Geom& g, const Shared<LY>& S
     x = x + tx;
     y = y + ty;
 }
-#endif
 
-#if SWARM_WALL_SPLIT
-// walls_dg with the 12 faces split over the 3 parts of a robot (SWARM_WALL_SPLIT). The first
-// read of the face table follows publish()'s exchange point (ordered after stage_tables).
-template <int LY>
-__device__ __forceinline__ void walls_dg_split(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
-    if (SWARM_ABLATE & 8) return;
-    float tx = 0.0f, ty = 0.0f;
-    if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int k = L.p + 3 * m;
-            const float4 f = S.face[k];
-            const float sda = fmaf(x, f.x, fmaf(y, f.y, f.z));
-            if (__any(sda < g.wall_clear_dg + 1e-4f)) {
-                const float2 q = S.facep[k];
-                const float sd = (x - q.x) * f.x + (y - q.y) * f.y;
-                const float pen = fmaxf(g.wall_clear_dg - sd, 0.0f);
-                tx += pen * f.x;
-                ty += pen * f.y;
-            }
-        }
-        if (__any(tx != 0.0f || ty != 0.0f)) {
-            S.wred[L.tid] = make_float2(tx, ty);
-            sync_wg<LY>();
-            const float2 a = S.wred[L.pbase], b = S.wred[L.pbase + 1], c = S.wred[L.pbase + 2];
-            tx = (a.x + b.x) + c.x;
-            ty = (a.y + b.y) + c.y;
-        }
-    }
-    x = x + tx;
-    y = y + ty;
-}
-#endif
 
 // MC:531-553 — sequential per face with the robot radius as clearance.
 __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
@@ -679,14 +497,6 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         float dx, dy;
         const float dd2 = sq_dist(x, y, pj.x, pj.y, dx, dy);
         (void)dd2;
-#if SWARM_PAIR_RSQ
-        const float s2 = fmaf(dx, dx, fmaf(dy, dy, 1e-8f));
-        const float rs = __builtin_amdgcn_rsqf(s2);
-        const float ov = fmaf(-s2, rs, g.min_dist);      // min_dist - dist
-        if (!(ov > 0.0f)) return;
-        const float hh = ov * rs * 0.5f;
-        const float hx = hh * dx, hy = hh * dy;
-#else
         const float dist = nsqrt(dd2 + 1e-8f);
         const float ov = g.min_dist - dist;
         if (!(ov > 0.0f)) return;
@@ -697,7 +507,6 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         // not branched: the other sums add +0, which leaves them unchanged (a sum
         // that starts at +0 never becomes -0 under round-to-nearest).
         const float hx = ov * nx * 0.5f, hy = ov * ny * 0.5f;
-#endif
         const bool row = j > L.i;
         rx += row ? hx : 0.0f;
         ry += row ? hy : 0.0f;
@@ -891,19 +700,8 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     //         walls, internal(none), gate, {push, walls, internal(i == 4 ? none : before), gate} i = 0..4, no push at i = 4
     constexpr bool INTERNAL = (MISSION == DIRGATE || MISSION == SHELTERING);
     constexpr bool apply = APPLY;
-#if SWARM_WALL_NEAR
     const int wfaces = wall_faces<LY>(S, x, y);
 #define SOLVE_WALLS() walls_dg_near<LY>(g, S, wfaces, x, y)
-#elif SWARM_WALL_SPLIT
-    constexpr bool WSPLIT = ly_parts(LY) == 3 && ly_waves(LY) == 1;
-#define SOLVE_WALLS()                                        \
-    do {                                                     \
-        if constexpr (WSPLIT) walls_dg_split<LY>(g, L, S, x, y); \
-        else walls_dg(g, x, y);                              \
-    } while (0)
-#else
-#define SOLVE_WALLS() walls_dg(g, x, y)
-#endif
     SOLVE_WALLS();
     if constexpr (INTERNAL) {
         if (!apply) capsules(g, x, y, false, 0.0f, 0.0f);
@@ -1012,7 +810,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         for (int s = 0; s < 32; s += ly_parts(LY)) m |= 1u << s;
         return m;
     }();
-#if SWARM_FACE_SPLIT
     if constexpr (ly_parts(LY) == 3 && ly_waves(LY) == 1) {
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -1022,7 +819,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             near_mask |= sda < g.prox_range + 1e-3f + 1e-4f ? (1u << s) : 0u;
         }
     } else
-#endif
     {
 #pragma unroll
         for (int s = 0; s < 12; ++s) {
@@ -1059,27 +855,11 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         SWARM_WT(L.wt_seg++);
         const int s = __builtin_ctz(near_mask);
         near_mask &= near_mask - 1u;
-#if SWARM_SEG_LDS
-        const float4 sg = S.seg[s];
-        const float ax = sg.x, ay = sg.y, sx = sg.z, sy = sg.w;
-#else
         const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
-#endif
         const float qx = ax - x, qy = ay - y;
-#if SWARM_RAY_PREFILTER
-        const float qs = qx * sy - qy * sx;
-#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float den = rdx[k] * sy - rdy[k] * sx;
-#if SWARM_RAY_PREFILTER
-            // t = qs / den (via v_rcp of den + 1e-12, within 1e-4 relative of 1 / den for
-            // |den| > 1e-8): t >= 0 needs qs, den of one sign, t <= range needs |qs| <= range |den|
-            // (a 1e-3 margin covers the reciprocal's rounding)
-            if (!__any((fabsf(den) > 1e-8f) & (qs * den >= 0.0f) &
-                       (fabsf(qs) <= g.prox_range * 1.001f * fabsf(den))))
-                continue;
-#endif
             const bool valid = fabsf(den) > 1e-8f;
             const float dd = den + 1e-12f;
             const float inv = frcp(dd);
@@ -1177,7 +957,7 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
         sx += raw * g.cos_a[k];
         sy += raw * g.sin_a[k];
     }
-    if (!need_agg) return;   // the cache aggregates are not read in this substep (SWARM_LAST_CACHE)
+    if (!need_agg) return;   // the cache aggregates are not read in this substep
     const float ang = atan2f(sy, sx);
     const bool above = mx > g.light_thr;
     lv = above ? mx : 0.0f;
@@ -1190,7 +970,7 @@ __device__ __forceinline__ void light(const Geom& g, float x, float y, float cyw
 // (Philox stream `purpose`, one block per 5 neighbours).
 template <int C>
 __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const float2* xy, const int* insv,
-                                            const float4* seg, float x,
+                                            float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
                                             uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy,
                                             const uint32_t* pre_cand = nullptr, const uint4* pre_rb = nullptr) {
@@ -1206,29 +986,18 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         // not strictly inside the convex arena; internal walls are always tested.
         const bool test_arena = !(me_in && insv[L.ab + j] != 0);
         const int s0 = test_arena ? 0 : 12;
-#if SWARM_RAB_FAST
         // pre_cand is the exact range test (obs_masks); without it (rab_only) test here
         const float s2 = dx * dx + dy * dy + 1e-8f;
         if (!pre_cand && !(s2 < g.rab_s_lim)) return;
         float dist = s2 * __builtin_amdgcn_rsqf(s2);
         if (s0 < g.nseg) dist = nsqrt(s2);
-#else
-        const float dist = nsqrt(dx * dx + dy * dy + 1e-8f);
-        if (!(dist < g.rab_range)) return;
-#endif
         bool blocked = false;
         // no segment to test (convex arena only, both ends strictly inside): skip the divisions
         if (s0 < g.nseg) {
         const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
         for (int s = s0; s < g.nseg; ++s) {
-#if SWARM_SEG_LDS
-            const float4 sg = seg[s];
-            const float sx = sg.z, sy = sg.w;
-            const float qx = sg.x - x, qy = sg.y - y;
-#else
             const float sx = g.seg_sx[s], sy = g.seg_sy[s];
             const float qx = g.seg_ax[s] - x, qy = g.seg_ay[s] - y;
-#endif
             const float den = rdx * sy - rdy * sx;
             const float dd = den + 1e-12f;
             const float t = (qx * sy - qy * sx) / dd;
@@ -1247,11 +1016,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         const float hb2 = bx * bx + by * by;
         float cb = 1.0f, sb = 0.0f;
         if (hb2 > 0.0f) {
-#if SWARM_RAB_FAST
             const float ih = __builtin_amdgcn_rsqf(hb2);
-#else
-            const float ih = frcp(fsqrt(hb2));
-#endif
             cb = bx * ih;
             sb = by * ih;
         }
@@ -1589,18 +1354,14 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
-        rab_partial<C>(g, L, S.xy, S.ins, SEG_LDS_PTR(S), x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
+        rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
                        FUSE ? &mrab : nullptr, FUSE ? &rb : nullptr);
     SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
     if (need_agg) proximity_aggregate(g, prox, agg.pv, agg.pa);
     light<MISSION>(g, x, y, cyw, syw, lt, agg.lv, agg.la, need_agg);
-#if SWARM_ZT_TABLE
     rab_finish(g, n, wx, wy, zt, r4, S.zt);
-#else
-    rab_finish(g, n, wx, wy, zt, r4);
-#endif
     agg.ax = axx;
     agg.ay = ayy;
     if (L.valid && obs) {
@@ -1637,7 +1398,7 @@ __device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<LY
                                          float cyw, const float* u_replay, uint64_t tick, float& ax, float& ay) {
     publish<LY>(g, L, S, x, y);
     float n, wx, wy;
-    rab_partial<C>(g, L, S.xy, S.ins, SEG_LDS_PTR(S), x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax,
+    rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_DISPATCH, tick, n, wx, wy, ax,
                    ay);
     combine<LY, C>(L, S, false, nullptr, n, wx, wy, ax, ay);
 }
@@ -1973,9 +1734,9 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         trunc_acc |= tout;
 
         // ---------------------------- observation ----------------------------
-        // SWARM_LAST_CACHE: with continuous actions (Isaac profile) the cache aggregates are only
+        // with continuous actions (Isaac profile) the cache aggregates are only
         // stored at the end of the launch; nothing reads them in between
-        const bool need_agg = !SWARM_LAST_CACHE || DISCRETE || PROFILE == STANDALONE || s == n_sub - 1;
+        const bool need_agg = DISCRETE || PROFILE == STANDALONE || s == n_sub - 1;
         observe<MISSION, PROFILE, LY, C>(g, L, S, x, y, yaw, u_obs, tick, out.obs, cache, syaw, cyaw, need_agg);
     }
 
