@@ -35,9 +35,10 @@ def main(src: str, dst: str, note: str = ""):
         "source": note or f"pytest -m gpu on MI355X (tests/parity.py record_stats), {src}",
         "rule": ("discrete outputs exact unless a 1-ulp input perturbation flips them; fp32 |got-ref| <= "
                  "1e-5*scale + 4*min(spread, 1e-3); elements with spread > 1e-3 (a discontinuity or sqrt "
-                 "singularity within one ulp) may instead pass if both values lie in the hull of the oracle's "
-                 "perturbed outputs (+-1e-5*scale); the proximity aggregate angle may pass as a vector "
-                 "(8e-5); angles mod 2 pi"),
+                 "singularity within one ulp) may instead pass only if each value is within 1e-5*scale of one "
+                 "of the oracle's own outputs (unperturbed, or under one of the 1-ulp input / libm "
+                 "perturbations: yaw, positions, all libm results, sin / cos alone or opposed); the "
+                 "proximity aggregate angle may pass as a vector (8e-5); angles mod 2 pi"),
         "groups": groups,
         "per_test": rows,
     }
