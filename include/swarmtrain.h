@@ -180,9 +180,11 @@ int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logi
 
 /* The learned-option (OC2) update's termination, option-selection and attention terms (agents/
  * learned_option_critic_trainer.py:1050-1093, 1140-1169, 1282-1322, 956-997; csrc/swarm_oc2terms.hip
- * states every formula). Each forward is one workgroup writing device scalars (denominators: the
- * given device scalar, or the local active count clamped to >= 1; the one used is returned for the
- * backward); each backward is elementwise and reads its incoming gradients from a device array.
+ * states every formula). Each forward writes device scalars (the attention and option forwards
+ * reduce over many workgroups into a library buffer, then add the workgroups' sums in a fixed order:
+ * one stream at a time; denominators: the given device scalar, or the local active count clamped to
+ * >= 1; the one used is returned for the backward); each backward is elementwise and reads its
+ * incoming gradients from a device array.
  *   termination: out[8] = loss, prior loss, entropy, mean beta, mean advantage, mean signal, low /
  *     high saturation over M rows of logits / advantages / term_mask (f32); grads[3] = d/d out[0..2];
  *   option terms (epsilon-greedy manager, forward only): out[5] = sum log_prob, option entropy,

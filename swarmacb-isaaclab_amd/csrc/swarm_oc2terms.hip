@@ -59,6 +59,63 @@ constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
 constexpr int kBwdThreads = 256;
 
+// Multi-block forwards (attention, option terms): block b writes its K partial sums to row b of
+// this buffer, then one finalising workgroup adds the rows in block order (a fixed order, so the
+// result does not depend on scheduling: graph replays equal eager runs bit for bit). One stream
+// at a time uses it (the trainer's update stream).
+constexpr int kPartBlocks = 2048;
+constexpr int kPartK = 24;
+__device__ float g_part[kPartBlocks * kPartK];
+constexpr int kPartThreads = 256;
+
+// block-wide sum of K per-thread partials over an NT-thread block; the result is valid in thread 0
+template <int K, int NT>
+__device__ __forceinline__ void block_sum_nt(float (&v)[K]) {
+    constexpr int W = NT / 64;
+    __shared__ float red[K][W];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) red[k][w] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            float s = 0.0f;
+            for (int i = 0; i < W; ++i) s += red[k][i];
+            v[k] = s;
+        }
+    }
+}
+
+// the K column sums of g_part rows [0, G), each in block order, into sums[K] (thread k < K of one
+// 64-thread workgroup: sequential, so the order is fixed)
+template <int K>
+__device__ __forceinline__ void part_sums(int G, float* sums) {
+    __shared__ float col[K];
+    const int k = threadIdx.x;
+    if (k < K) {
+        float s = 0.0f;
+        for (int b = 0; b < G; ++b) s += g_part[b * kPartK + k];
+        col[k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) sums[i] = col[i];
+    }
+}
+
+__host__ __device__ constexpr int part_blocks(int64_t rows) {
+    return (int)(rows / kPartThreads + 1 < kPartBlocks ? rows / kPartThreads + 1 : kPartBlocks);
+}
+
 // block-wide sum of K per-thread partials; the result is valid in thread 0
 template <int K>
 __device__ __forceinline__ void block_sum(float (&v)[K]) {
@@ -138,46 +195,64 @@ __global__ __launch_bounds__(kBwdThreads) void term_bwd_kernel(int64_t M, const 
 // ------------------------------------------------------------------- option selection
 constexpr int kMaxOptions = 16;
 
-__global__ __launch_bounds__(kThreads) void option_fwd_kernel(int64_t M, int O, const float* __restrict__ q,
-                                                              const int64_t* __restrict__ options,
-                                                              const uint8_t* __restrict__ mask,
-                                                              const uint8_t* __restrict__ boundary,
-                                                              const float* denom_b, float low, float greedy_add,
-                                                              float log_o, float* __restrict__ out) {
-    // partials: sum log p[option], sum H boundary, sum boundary, sum mask, marginal numerators
-    float v[4 + kMaxOptions];
+// row partials: sum log p[option], sum H boundary, sum boundary, sum mask, marginal numerators
+__device__ __forceinline__ void option_row(int O, const float* r, int64_t opt, float bm, float mk, float lo, float hi,
+                                           float llo, float lhi, float (&v)[4 + kMaxOptions]) {
+    int best = 0;
+    float bq = r[0];
+    for (int o = 1; o < O; ++o)
+        if (r[o] > bq) {   // torch.argmax: the first maximal entry
+            bq = r[o];
+            best = o;
+        }
+    v[0] += opt == best ? lhi : llo;
+    // entropy of the row: (O - 1) cells of lo, one of hi
+    float h = 0.0f;
+    for (int o = 0; o < O; ++o) h -= o == best ? hi * lhi : lo * llo;
+    v[1] += h * bm;
+    v[2] += bm;
+    v[3] += mk;
 #pragma unroll
-    for (int k = 0; k < 4 + kMaxOptions; ++k) v[k] = 0.0f;
+    for (int o = 0; o < kMaxOptions; ++o)
+        if (o < O) v[4 + o] += (o == best ? hi : lo) * mk;
+}
+
+__device__ __forceinline__ void option_probs(int O, float low, float greedy_add, float& lo, float& hi, float& llo,
+                                             float& lhi) {
     constexpr float kEps32 = 1.1920928955078125e-07f;   // torch.finfo(float32).eps (clamp_probs)
     const float hi0 = low + greedy_add;
     float tot = 0.0f;                                    // probs.sum(-1): (O - 1) x low + hi0
     for (int o = 0; o < O - 1; ++o) tot += low;
     tot += hi0;
-    const float lo = low / tot, hi = hi0 / tot;
-    const float llo = logf(fminf(fmaxf(lo, kEps32), 1.0f - kEps32)), lhi = logf(fminf(fmaxf(hi, kEps32), 1.0f - kEps32));
-    for (int64_t m = threadIdx.x; m < M; m += kThreads) {
-        const float* r = q + m * O;
-        int best = 0;
-        float bq = r[0];
-        for (int o = 1; o < O; ++o)
-            if (r[o] > bq) {   // torch.argmax: the first maximal entry
-                bq = r[o];
-                best = o;
-            }
-        const int64_t opt = options[m];
-        v[0] += opt == best ? lhi : llo;
-        // entropy of the row: (O - 1) cells of lo, one of hi
-        float h = 0.0f;
-        for (int o = 0; o < O; ++o) h -= o == best ? hi * lhi : lo * llo;
-        const float bm = boundary[m] ? 1.0f : 0.0f, mk = mask[m] ? 1.0f : 0.0f;
-        v[1] += h * bm;
-        v[2] += bm;
-        v[3] += mk;
+    lo = low / tot;
+    hi = hi0 / tot;
+    llo = logf(fminf(fmaxf(lo, kEps32), 1.0f - kEps32));
+    lhi = logf(fminf(fmaxf(hi, kEps32), 1.0f - kEps32));
+}
+
+__global__ __launch_bounds__(kPartThreads) void option_part_kernel(int64_t M, int O, const float* __restrict__ q,
+                                                                   const int64_t* __restrict__ options,
+                                                                   const uint8_t* __restrict__ mask,
+                                                                   const uint8_t* __restrict__ boundary, float low,
+                                                                   float greedy_add) {
+    float v[4 + kMaxOptions];
 #pragma unroll
-        for (int o = 0; o < kMaxOptions; ++o)
-            if (o < O) v[4 + o] += (o == best ? hi : lo) * mk;
+    for (int k = 0; k < 4 + kMaxOptions; ++k) v[k] = 0.0f;
+    float lo, hi, llo, lhi;
+    option_probs(O, low, greedy_add, lo, hi, llo, lhi);
+    for (int64_t m = (int64_t)blockIdx.x * kPartThreads + threadIdx.x; m < M; m += (int64_t)gridDim.x * kPartThreads)
+        option_row(O, q + m * O, options[m], boundary[m] ? 1.0f : 0.0f, mask[m] ? 1.0f : 0.0f, lo, hi, llo, lhi, v);
+    block_sum_nt<4 + kMaxOptions, kPartThreads>(v);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 4 + kMaxOptions; ++k) g_part[blockIdx.x * kPartK + k] = v[k];
     }
-    block_sum<4 + kMaxOptions>(v);
+}
+
+__global__ __launch_bounds__(64) void option_fin_kernel(int G, int O, const float* denom_b, float log_o,
+                                                        float* __restrict__ out) {
+    __shared__ float v[4 + kMaxOptions];
+    part_sums<4 + kMaxOptions>(G, v);
     if (threadIdx.x == 0) {
         const float nb = denom_b ? *denom_b : fmaxf(v[2], 1.0f);
         const float nm = fmaxf(v[3], 1.0f);
@@ -206,15 +281,15 @@ __device__ __forceinline__ float row_norm(const float* a, int D) {
     return fmaxf(sqrtf(s), 1e-8f);
 }
 
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(int B, int L, int O, int D, const float* __restrict__ att,
-                                                            const uint8_t* __restrict__ mask,
-                                                            const float* __restrict__ dones, const float* d_rows,
-                                                            const float* d_pairs, float* __restrict__ out,
-                                                            float* __restrict__ used) {
-    float v[5] = {0, 0, 0, 0, 0};   // diversity sum, temporal sum, attention sum, rows, pairs
+// row partials: diversity sum, temporal sum, attention sum, rows, pairs (one row per thread)
+__global__ __launch_bounds__(kPartThreads) void attn_part_kernel(int B, int L, int O, int D,
+                                                                 const float* __restrict__ att,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 const float* __restrict__ dones) {
+    float v[5] = {0, 0, 0, 0, 0};
     const int64_t rows = (int64_t)B * L;
     const int OD = O * D;
-    for (int64_t r = threadIdx.x; r < rows; r += kThreads) {
+    for (int64_t r = (int64_t)blockIdx.x * kPartThreads + threadIdx.x; r < rows; r += (int64_t)gridDim.x * kPartThreads) {
         const float* a = att + r * OD;
         const float act = mask[r] ? 1.0f : 0.0f;
         float inv[kMaxAttnO];
@@ -241,10 +316,21 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(int B, int L, int O,
             v[4] += pr;
         }
     }
-    block_sum<5>(v);
+    block_sum_nt<5, kPartThreads>(v);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) g_part[blockIdx.x * kPartK + k] = v[k];
+    }
+}
+
+__global__ __launch_bounds__(64) void attn_fin_kernel(int G, int O, int D, const float* d_rows, const float* d_pairs,
+                                                      float* __restrict__ out, float* __restrict__ used) {
+    __shared__ float v[5];
+    part_sums<5>(G, v);
     if (threadIdx.x == 0) {
         const float nr = d_rows ? *d_rows : fmaxf(v[3], 1.0f);
         const float np = d_pairs ? *d_pairs : fmaxf(v[4], 1.0f);
+        const int OD = O * D;
         out[0] = v[0] / (nr * (float)(O * (O - 1)));
         out[1] = v[1] / np;
         out[2] = v[2] / (nr * (float)OD);
@@ -419,8 +505,10 @@ int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values,
                                float low, float greedy_add, float log_num_options, float* out, void* stream) {
     if (M < 1 || O < 1 || O > kMaxOptions || !option_values || !options || !loss_mask || !boundary || !out)
         return SWARM_ERR_ARG;
-    option_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
-        M, O, option_values, options, loss_mask, boundary, boundary_denom, low, greedy_add, log_num_options, out);
+    const int G = part_blocks(M);
+    option_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(M, O, option_values, options,
+                                                                                 loss_mask, boundary, low, greedy_add);
+    option_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(G, O, boundary_denom, log_num_options, out);
     return status();
 }
 
@@ -430,8 +518,11 @@ int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, co
     if (B < 1 || L < 1 || O < 2 || O > kMaxAttnO || D < 1 || D > kMaxAttnD || !attentions || !loss_mask || !dones ||
         !out || !used_denoms || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
         return SWARM_ERR_ARG;
-    attn_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask, dones,
-                                                                          row_denom, pair_denom, out, used_denoms);
+    const int G = part_blocks((int64_t)B * L);
+    attn_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask,
+                                                                               dones);
+    attn_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(G, O, D, row_denom, pair_denom, out,
+                                                                    used_denoms);
     return status();
 }
 
