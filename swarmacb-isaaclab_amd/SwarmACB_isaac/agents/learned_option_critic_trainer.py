@@ -624,10 +624,14 @@ class LearnedOptionCriticTrainer(TrainerBase):
         with torch.no_grad():
             next_joint_memory = (batch["next_option_joint_memory_h"].reshape(B * L, -1).unsqueeze(0),
                                  batch["next_option_joint_memory_c"].reshape(B * L, -1).unsqueeze(0))
-            next_q = self.option_critic.joint_action_pass(flat_next_states, encoded,
-                                                          memory=next_joint_memory).squeeze(-1)
             alternatives = self.option_critic.focal_discrete_counterfactual_values(
                 flat_next_states, flat_joint_options, focal_ids, O, memory=next_joint_memory)
+            # Q(s', omega) with the focal robot's own option is the alternative at that option:
+            # the counterfactual row for it carries the same one-hot joint options, states and
+            # memory as the reference's separate joint_action_pass (LOT:1294-1298), so it is
+            # gathered instead of recomputed (one critic pass fewer per optimizer step)
+            focal_option = flat_joint_options.gather(1, focal_ids.long().unsqueeze(1))
+            next_q = alternatives.gather(1, focal_option.long()).squeeze(1)
             reselection = self.actor.option_state_value(next_option_values, alternatives,
                                                         epsilon=self.current_option_epsilon)
             termination_advantage = (next_q - reselection).view(B, L)

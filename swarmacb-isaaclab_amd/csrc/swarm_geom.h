@@ -70,7 +70,7 @@ enum RngPurpose : uint32_t {
     S(float, r_robot) S(float, min_dist) S(float, r2) S(float, max_speed) S(float, wheelbase) S(float, dt)  \
     S(float, min_dist2_hi) S(float, rab_range2_hi) S(float, inv_prox_range) S(float, inv_unity)             \
     /* exact squared thresholds: fl(sqrt(s)) < R  <=>  s < x_s_lim (smallest float whose sqrt reaches R) */  \
-    S(float, rab_s_lim)                                                                                     \
+    S(float, min_dist_s_lim) S(float, rab_s_lim)                                                            \
     S(float, prox_range) S(float, rab_range) S(float, rab_loss) S(float, unity) S(float, light_thr)         \
     S(float, light_int) S(float, alpha) S(float, prox_thr) S(float, pi_f) S(float, two_pi_f)                \
     S(float, half_pi_f) S(float, critic_radius)

@@ -235,6 +235,7 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     // float pre-filter a strict superset of the exact test (the kernels re-check).
     g.min_dist2_hi = (float)((double)g.min_dist * g.min_dist * (1.0 + 1.0 / 1048576.0));
     g.rab_range2_hi = (float)((double)g.rab_range * g.rab_range * (1.0 + 1.0 / 1048576.0));
+    g.min_dist_s_lim = sqrt_lim(g.min_dist);
     g.rab_s_lim = sqrt_lim(g.rab_range);
     g.inv_prox_range = 1.0f / g.prox_range;
     g.inv_unity = 1.0f / g.unity;

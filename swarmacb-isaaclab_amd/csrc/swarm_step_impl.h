@@ -491,15 +491,16 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     sync_wg<LY>();
     SWARM_PH_NEXT(L, PH_PUSH_PUB, wt_t);
     float rx = 0.0f, ry = 0.0f, cx = 0.0f, cy = 0.0f;
-    // candidate pairs from the squared distance (a superset: s >= md2_hi implies
-    // fl(sqrt(s)) >= min_dist), then the exact sqrt test only for candidates
-    auto pair_term = [&](int j, float2 pj) {
+    // Contact pairs from the squared distance. The chunk path's mask is exact: s < min_dist_s_lim
+    // (the smallest float whose correctly rounded sqrt reaches min_dist) is fl(sqrt(s)) < min_dist,
+    // i.e. ov > 0, so its pair terms need no test; the generic path's mask is a superset
+    // (s >= md2_hi implies fl(sqrt(s)) >= min_dist) and tests each candidate.
+    auto pair_term = [&](int j, float2 pj, bool exact) {
         float dx, dy;
         const float dd2 = sq_dist(x, y, pj.x, pj.y, dx, dy);
-        (void)dd2;
         const float dist = nsqrt(dd2 + 1e-8f);
         const float ov = g.min_dist - dist;
-        if (!(ov > 0.0f)) return;
+        if (!exact && !(ov > 0.0f)) return;
         const float inv = frcp(dist + 1e-8f);
         const float nx = dx * inv, ny = dy * inv;
         // row term of pair (i, j) if j > i, else the column term of pair (j, i)
@@ -517,12 +518,12 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
         const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float px, float py) {
             float dx, dy;
-            return sq_dist(px, py, x, y, dx, dy) + 1e-8f < g.min_dist2_hi;
+            return sq_dist(px, py, x, y, dx, dy) + 1e-8f < g.min_dist_s_lim;
         }, true);
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
-            pair_term(j, p);
+            pair_term(j, p, true);
         });
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
     } else {
@@ -539,7 +540,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         while (cand) {
             const int j = __builtin_ctzll(cand);
             cand &= cand - 1ull;
-            pair_term(j, S.xy[L.ab + j]);
+            pair_term(j, S.xy[L.ab + j], false);
         }
     }
     if constexpr (ly_parts(LY) > 1) {
