@@ -357,7 +357,11 @@ def lstm_sequences(items):
     groups: dict = {}
     for i, item in enumerate(items):
         lstm, seq, state, keep = item[:4]
-        if _fused_seq_ok(lstm, seq):
+        if _fused_seq_ok(lstm, seq) and seq.shape[1] == 1 and seq.shape[0] >= SINGLE_STEP_ROWS:
+            frozen = len(item) > 4 and item[4]
+            with torch.no_grad() if frozen else contextlib.nullcontext():
+                out[i] = _lstm_single_step(lstm, seq, state)
+        elif _fused_seq_ok(lstm, seq):
             groups.setdefault((seq.shape[1], lstm.hidden_size, seq.device), []).append(i)
         else:
             frozen = len(item) > 4 and item[4]
@@ -385,6 +389,26 @@ def lstm_sequences(items):
                     h_seq, c_n = h_seq.detach(), c_n.detach()
                 out[i] = (h_seq, (h_seq[:, -1].unsqueeze(0), c_n.unsqueeze(0)))
     return out
+
+
+# One-step recurrences over at least this many rows (the OC2 update's next-state actor pass:
+# 2,048 manager rows and 12,288 option rows per C5 minibatch) leave the whole-sequence kernel,
+# whose workgroup per row loads its gate rows of W_hh for a single step (449 us for the 12,288
+# option rows), for two library GEMMs and the cell's elementwise terms (autograd-capable).
+SINGLE_STEP_ROWS = 512
+
+
+def _lstm_single_step(lstm: nn.LSTM, seq: torch.Tensor, state):
+    """lstm(seq, state) for T = 1 (nn.LSTM's gate order i, f, g, o). A keep mask acts only
+    between steps, so a single step has none to apply."""
+    n, units = seq.shape[0], lstm.hidden_size
+    gates = torch.addmm(torch.nn.functional.linear(seq.reshape(n, -1), lstm.weight_ih_l0,
+                                                   lstm.bias_ih_l0 + lstm.bias_hh_l0),
+                        state[0].reshape(n, units), lstm.weight_hh_l0.t())
+    i, f, g, o = gates.chunk(4, dim=1)
+    c1 = torch.sigmoid(f) * state[1].reshape(n, units) + torch.sigmoid(i) * torch.tanh(g)
+    h1 = torch.sigmoid(o) * torch.tanh(c1)
+    return h1.view(n, 1, units), (h1.view(1, n, units), c1.view(1, n, units))
 
 
 def _lstm_loop(lstm: nn.LSTM, seq: torch.Tensor, state, keep: torch.Tensor | None = None):

@@ -3,9 +3,9 @@
 //
 // One 256-thread workgroup per sequence walks all T steps: the forward keeps
 // its gate row of W_hh in registers (thread j = gate pre-activation j, up to
-// 4 x 64 units) and the carried (masked) h in lane u of every wave, so a step is
-// U scalar broadcasts, one register dot product, one activation, one barrier and
-// one cell update; the backward keeps
+// 4 x 64 units) and the carried (masked) h in lane u of every wave plus a per-wave LDS
+// row, so a step is one LDS-broadcast dot product (packed FMAs), one activation, one
+// barrier and one cell update; the backward keeps
 // the W_hh^T slice it needs in registers and walks the steps in reverse. A
 // minibatch of the ML-Agents trainers (16 sequences x 128 steps) is then one
 // launch instead of 128 library LSTM calls (forward) plus 128 (backward).
@@ -91,17 +91,42 @@ __device__ __forceinline__ float lane_bcast(float v, int k) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// sum_k w[k] v[k] over the wave's LDS row v (KU floats, 16-byte aligned), as four chains
+// k = 0, 1, 2, 3 (mod 4) combined ((a0 + a1) + (a2 + a3)); the chain pairs run as packed FMAs
+// (v_pk_fma_f32) on same-address float4 reads (an LDS broadcast)
+template <int KU>
+__device__ __forceinline__ float row_dot_lds(const float (&w)[KU], const float* v) {
+    static_assert(KU % 4 == 0, "packed chains need KU % 4 == 0");
+    const float4* v4 = reinterpret_cast<const float4*>(v);
+    f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < KU; k += 4) {
+        const float4 h = v4[k / 4];
+        a01 = __builtin_elementwise_fma((f32x2){w[k], w[k + 1]}, (f32x2){h.x, h.y}, a01);
+        a23 = __builtin_elementwise_fma((f32x2){w[k + 2], w[k + 3]}, (f32x2){h.z, h.w}, a23);
+    }
+    return (a01.x + a01.y) + (a23.x + a23.y);
+}
+
 // Forward: NT = 256 threads = 4 waves per sequence, thread j = gate row j. Every wave
-// computes all U cell updates itself (lane u = unit u), so h_u sits in lane u of EVERY
-// wave and a gate row's product with h reads it by v_readlane into scalar registers:
-// no LDS round trip for h. The gates of a step go through one LDS buffer (double-buffered
-// by step parity) and ONE barrier. Per step: U readlanes + U FMAs (4 chains) per lane,
-// one activation, one LDS write / barrier / read, one cell update.
+// computes all U cell updates itself (lane u = unit u) and keeps its own copy of h in an LDS
+// row, so a gate row's product with h needs only a wavefront fence, no barrier: 16
+// same-address float4 reads and 32 packed FMAs per step (the 64 v_readlane_b32 + 64 FMAs of
+// round 3 gave bitwise the same sums 5-20 % slower, profiles/r04/train/lstm_ab_*.jsonl). The
+// gates of a step go through one LDS buffer (double-buffered by step parity) and ONE barrier.
 template <int UC, bool KEEP>
 __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const Batch<FwdSeq> bt) {
     constexpr int KU = UC > 0 ? UC : MAXU;              // register extent of a gate row
     const int U = UC > 0 ? UC : U_rt;
     __shared__ __attribute__((aligned(16))) float gs[2][4 * MAXU];
+    __shared__ __attribute__((aligned(16))) float hs[NT / 64][MAXU];   // each wave's copy of h
     const int item = batch_item(bt, blockIdx.x);
     const FwdSeq& sq = bt.s[item];
     const float* __restrict__ xg = sq.xg;
@@ -125,6 +150,8 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
     const bool unit = lane < U;                          // lane u = unit u in every wave
     float c = unit ? c0[b * U + lane] : 0.0f;
     float h = unit ? h0[b * U + lane] : 0.0f;            // 0 in lanes >= U (their w columns are 0 too)
+    hs[wave][lane] = h;
+    wave_sync();
     const int kind = jc / U;                             // 0 i, 1 f, 2 g, 3 o
     const float* xb = xg + b * T * G + jc;
     auto load_group = [&](int t0, float* xr, float* kr) {
@@ -146,21 +173,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
             if (t >= T) break;
             const int64_t row = b * T + t;
             float* g = gs[t & 1];
-            // all U broadcasts first (scalar registers), then the products: a readlane's
-            // result read by the very next VALU instruction costs wait states
-            float hk[KU];
-#pragma unroll
-            for (int k = 0; k < KU; ++k) hk[k] = lane_bcast(h, k);
-            __builtin_amdgcn_sched_barrier(0);
-            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-#pragma unroll
-            for (int k = 0; k < KU; k += 4) {
-                a0 = fmaf(w[k], hk[k], a0);
-                if (k + 1 < KU) a1 = fmaf(w[k + 1], hk[k + 1], a1);
-                if (k + 2 < KU) a2 = fmaf(w[k + 2], hk[k + 2], a2);
-                if (k + 3 < KU) a3 = fmaf(w[k + 3], hk[k + 3], a3);
-            }
-            const float a = ((a0 + a1) + (a2 + a3)) + xr[p];
+            const float a = row_dot_lds<KU>(w, hs[wave]) + xr[p];
             float v;
             if (kind == 2)   // wave-uniform for 64 units (wave q = gate q)
                 v = act_tanh(a);
@@ -183,6 +196,8 @@ __global__ void __launch_bounds__(NT) lstm_seq_fwd_kernel(int T, int U_rt, const
                 h *= kk;
                 c *= kk;
             }
+            hs[wave][lane] = h;   // 0 in lanes >= U
+            wave_sync();
         }
 #pragma unroll
         for (int p = 0; p < PF; ++p) {

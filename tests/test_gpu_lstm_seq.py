@@ -45,7 +45,8 @@ def _run(fused, lstm, x, h0, c0, keep, wout):
 
 @pytest.mark.parametrize("n,T,inp,units,masked", [(16, 128, 128, 64, True), (16, 128, 128, 64, False),
                                                   (96, 128, 128, 64, False), (5, 7, 16, 8, True),
-                                                  (12288, 1, 128, 32, False), (3, 2, 4, 1, True)])
+                                                  (12288, 1, 128, 32, False), (2048, 1, 64, 64, True),
+                                                  (511, 1, 64, 64, False), (3, 2, 4, 1, True)])
 def test_lstm_sequence_matches_torch(gpu_device, n, T, inp, units, masked):
     case = _case(n, T, inp, units, masked, gpu_device)
     outs_k, grads_k = _run(True, *case)
