@@ -34,9 +34,13 @@ typedef enum {
     SWARM_RSA_SINGLE_OF_PAIRS = 2, /* one set per env from the BASELINES layout: entities = rows 0 .. N-1
                                  of each env's 2N-row block, so the team value V(s) (critic_pass) and
                                  the baselines of one decision share one embedding / projection pass */
-    SWARM_RSA_ACTIONS_OF_PAIRS = 3 /* one set per env from the BASELINES layout: entities = rows N .. 2N-1
+    SWARM_RSA_ACTIONS_OF_PAIRS = 3, /* one set per env from the BASELINES layout: entities = rows N .. 2N-1
                                  (the state+action rows), i.e. joint_action_pass's Q(s, a) — the
                                  option-critic trainers' collective option value shares the pass too */
+    SWARM_RSA_FOCAL = 4       /* A sets per env (swarm_rsa_pool_focal only): R = N + A rows per env,
+                                 0..N-1 the joint state+option entities, N..N+A-1 the focal robot's
+                                 entity under each of its A alternatives; set a = rows 0..N-1 with
+                                 row focal[b] replaced by row N + a (increasing member order) */
 } swarm_rsa_mode_t;
 
 /* pooled[(b * n_sets + s) * hidden + c] = mean over the N members of set s of
@@ -48,6 +52,17 @@ typedef enum {
  * (v_mfma_f32_16x16x4_f32: exact fp32 products). x, qkv and pooled must be 16-byte aligned. */
 int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_t hidden, const float* x,
                        const float* qkv, const float* w_out, const float* b_out, float* pooled, void* stream);
+
+/* swarm_rsa_pool for SWARM_RSA_FOCAL: the focal counterfactual values of the OC2 termination
+ * advantage (POCACritic.focal_discrete_counterfactual_values, reference poca_networks.py:715-762,
+ * called from learned_option_critic_trainer.py:1299-1306). The reference embeds and attends
+ * B * A full sets of N entities; here the N joint rows and the A alternative rows of an env are
+ * embedded and projected ONCE and the attention logits of all (N + A)^2 row pairs are shared by
+ * its A sets. pooled[(b * A + a) * hidden + c]; focal: [B] int64 in [0, N) (clamped on the device).
+ * Supported: hidden = 128, heads in {1, 2, 4}, 1 <= N <= 20, 1 <= A, N + A <= 40. */
+int32_t swarm_rsa_pool_focal(int32_t B, int32_t N, int32_t A, int32_t heads, int32_t hidden, const float* x,
+                             const float* qkv, const float* w_out, const float* b_out, const int64_t* focal,
+                             float* pooled, void* stream);
 
 /* out[r][c] = (in[r][c] - mean_r) / sqrt(var_r + 1e-5) over the hidden = 128 features of each of the
  * `rows` rows (biased variance): the entity-embedding LayerNorm (no affine) that produces x above,

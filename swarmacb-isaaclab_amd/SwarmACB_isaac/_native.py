@@ -69,7 +69,7 @@ class GatherField(C.Structure):
 
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
-CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
+CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_pool_focal", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
                  "swarm_rsa_attn_backward", "swarm_tensor_list_copy", "swarm_lstm_seq_forward_batch",
                  "swarm_lstm_seq_backward_batch", "swarm_row_norm_forward", "swarm_row_norm_backward",
@@ -94,7 +94,8 @@ class LstmSeqBwd(C.Structure):
 ATTN_MAX_ENTITIES = 32
 ATTN_HEAD_DIMS = (32, 64, 128)
 LSTM_SEQ_MAX_UNITS = 64
-RSA_SINGLE, RSA_BASELINES, RSA_SINGLE_OF_PAIRS, RSA_ACTIONS_OF_PAIRS = 0, 1, 2, 3
+RSA_SINGLE, RSA_BASELINES, RSA_SINGLE_OF_PAIRS, RSA_ACTIONS_OF_PAIRS, RSA_FOCAL = 0, 1, 2, 3, 4
+RSA_MAX_ROWS = 40   # N + alternatives of swarm_rsa_pool_focal
 
 RECORD_MAX_MEMORIES = 12
 
@@ -164,6 +165,8 @@ def load() -> C.CDLL:
     lib.swarm_decision_record.argtypes = [i32, i32, C.c_double, vp, vp, vp, vp, C.POINTER(DecisionRecord), vp]
     lib.swarm_rsa_pool.restype = i32
     lib.swarm_rsa_pool.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
+    lib.swarm_rsa_pool_focal.restype = i32
+    lib.swarm_rsa_pool_focal.argtypes = [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_rsa_embedding_norm.restype = i32
     lib.swarm_rsa_embedding_norm.argtypes = [C.c_int64, i32, vp, vp, vp]
     lib.swarm_lstm_cell.restype = i32

@@ -825,6 +825,8 @@ class POCACritic(nn.Module):
         """Q for every alternative of one focal agent per row (poca_networks.py:715-762)."""
         B, N, _ = all_agent_states.shape
         dev = all_agent_states.device
+        if self._fused(all_agent_states, N) and N + num_actions <= _native.RSA_MAX_ROWS and B > 0:
+            return self._focal_values_shared(all_agent_states, action_indices, focal_agent_ids, num_actions, memory)
         idx = action_indices.unsqueeze(1).expand(B, num_actions, N).clone()
         idx[torch.arange(B, device=dev).unsqueeze(1), torch.arange(num_actions, device=dev).unsqueeze(0),
             focal_agent_ids.long().unsqueeze(1).expand(-1, num_actions)] = \
@@ -838,6 +840,45 @@ class POCACritic(nn.Module):
             mem = tuple(m.unsqueeze(2).expand(-1, -1, num_actions, -1).reshape(m.shape[0], B * num_actions,
                                                                                m.shape[-1]) for m in memory)
         return self.joint_action_pass(states, onehot, memory=mem).reshape(B, num_actions)
+
+    def _focal_values_shared(self, all_agent_states, action_indices, focal_agent_ids, num_actions: int, memory):
+        """focal_discrete_counterfactual_values without re-embedding the A copies of each row's
+        set: the N joint entities and the focal robot's A alternative entities are embedded once
+        (A + N rows per row, instead of A * N) and swarm_rsa_pool_focal attends the A sets over
+        them, sharing the projections and the logits of the row (no-grad, the termination
+        advantage's pass). Same sets, same member order as the reference's; only the summation
+        order of the shared products differs (float32 rounding)."""
+        B, N, S = all_agent_states.shape
+        A = num_actions
+        dev = all_agent_states.device
+        focal = focal_agent_ids.long().reshape(B)
+        onehot = torch.nn.functional.one_hot(action_indices.long(), num_classes=A).to(all_agent_states.dtype)
+        focal_state = all_agent_states[torch.arange(B, device=dev), focal]
+        alt = torch.cat([focal_state.unsqueeze(1).expand(B, A, S),
+                         torch.eye(A, dtype=all_agent_states.dtype, device=dev).unsqueeze(0).expand(B, A, A)], dim=-1)
+        rows = self.obs_act_entity_enc(torch.cat([torch.cat([all_agent_states, onehot], dim=-1), alt], dim=1))
+        rows = rows.contiguous()
+        attn = self.self_attn
+        x = torch.empty_like(rows)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _native.check(lib.swarm_rsa_embedding_norm(rows.numel() // attn.embed_dim, attn.embed_dim,
+                                                   C.c_void_p(rows.data_ptr()), C.c_void_p(x.data_ptr()), stream),
+                      "swarm_rsa_embedding_norm")
+        w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
+        b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
+        qkv = torch.nn.functional.linear(x, w, b).contiguous()
+        wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
+        focal = focal.contiguous()
+        pooled = torch.empty(B * A, attn.embed_dim, dtype=torch.float32, device=dev)
+        _native.check(lib.swarm_rsa_pool_focal(B, N, A, attn.num_heads, attn.embed_dim, C.c_void_p(x.data_ptr()),
+                                               C.c_void_p(qkv.data_ptr()), C.c_void_p(wo.data_ptr()),
+                                               C.c_void_p(bo.data_ptr()), C.c_void_p(focal.data_ptr()),
+                                               C.c_void_p(pooled.data_ptr()), stream), "swarm_rsa_pool_focal")
+        mem = None
+        if memory is not None:
+            mem = tuple(m.unsqueeze(2).expand(-1, -1, A, -1).reshape(m.shape[0], B * A, m.shape[-1]) for m in memory)
+        return self._value_tail(pooled, N, mem).reshape(B, A)
 
     def baseline(self, agent_i_state, other_states, other_actions, memory=None, sequence_length: int = 1,
                  return_memory: bool = False):

@@ -80,6 +80,8 @@ constexpr int SINGLE_ENVS = RMAX / NMAX;
 
 // entity row of member k of set s (swarm_rsa_mode_t); in SINGLE mode set s is
 // the s-th env staged in this iteration
+// (FOCAL, the FOC instantiation of rsa_pool_kernel: set s of the env is its N joint rows with
+// row f, the focal robot's, replaced by alternative row N + s)
 __device__ __forceinline__ int member(int mode, int N, int s, int k) {
     if (mode != SWARM_RSA_BASELINES) return s * N + k;
     return k == 0 ? s : N + (k - 1 < s ? k - 1 : k);
@@ -89,14 +91,17 @@ __device__ __forceinline__ int member(int mode, int N, int s, int k) {
 // runtime n_rt. A compile-time set size lets every per-member loop unroll
 // without predicates, so the LDS reads of a loop are all in flight at once:
 // with two waves per SIMD little else hides their latency.
-template <int NH, int NC>
+template <int NH, int NC, bool FOC = false>
 __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt, const float* __restrict__ X,
                                                        const float* __restrict__ QKV, const float* __restrict__ Wo,
-                                                       const float* __restrict__ bo, float* __restrict__ pooled) {
+                                                       const float* __restrict__ bo, float* __restrict__ pooled,
+                                                       const int64_t* __restrict__ focal = nullptr, int n_alt = 0) {
     const int N = NC > 0 ? NC : n_rt;
     constexpr int DH = HD / NH;   // head width
-    const bool single = mode != SWARM_RSA_BASELINES;
-    const int erows = mode == SWARM_RSA_SINGLE ? N : 2 * N;   // entity rows per env in memory
+    constexpr bool foc = FOC;   // SWARM_RSA_FOCAL
+    const bool single = mode != SWARM_RSA_BASELINES && !foc;
+    const int env_sets = foc ? n_alt : N;                      // sets per env (BASELINES / FOCAL)
+    const int erows = mode == SWARM_RSA_SINGLE ? N : foc ? N + n_alt : 2 * N;   // entity rows per env in memory
     const int roff = mode == SWARM_RSA_ACTIONS_OF_PAIRS ? N : 0;  // first staged row of an env's block
     const int iters = single ? (B + SINGLE_ENVS - 1) / SINGLE_ENVS : B;
 
@@ -134,11 +139,17 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
         // envs of this iteration (rows of consecutive envs are contiguous), their
         // entity rows and sets, and the first output row
         const int e0 = single ? it * SINGLE_ENVS : it;
-        const int n_sets = single ? min(SINGLE_ENVS, B - e0) : N;
-        const int R = single ? n_sets * N : 2 * N;   // = the rows of a set group
+        const int n_sets = single ? min(SINGLE_ENVS, B - e0) : env_sets;
+        const int R = single ? n_sets * N : erows;   // = the rows of a set group
         const int groups = single ? n_sets : 1;      // blocks of rows that attend to each other
         const int G = R / groups;
-        const size_t out0 = single ? (size_t)e0 : (size_t)e0 * N;
+        const size_t out0 = single ? (size_t)e0 : (size_t)e0 * env_sets;
+        int fr = 0;   // the focal row (FOCAL)
+        if constexpr (FOC) fr = (int)min<int64_t>(max<int64_t>(focal[e0], 0), N - 1);
+        auto mem = [&](int s_, int k) {
+            if constexpr (FOC) return k == fr ? N + s_ : k;
+            else return member(mode, N, s_, k);
+        };
         // ---- phase 0: x, q, k, v rows of this iteration
         // (SINGLE_OF_PAIRS: staged row r is row r % N of env e0 + r / N's 2N-row block;
         //  ACTIONS_OF_PAIRS: row N + r % N of that block)
@@ -197,13 +208,13 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
             if (have && !(RSA_ABLATE & 2)) {
                 for (int p = lane + 64 * half; p < N * NH; p += 128) {
                     const int r = p / NH, h = p - (p / NH) * NH;
-                    const float* srow = &S[h * SHS + member(mode, N, set, r) * SW];
+                    const float* srow = &S[h * SHS + mem(set, r) * SW];
                     float l[NMAX];
                     float m = -INFINITY;
 #pragma unroll
                     for (int k = 0; k < NMAX; ++k)
                         if (k < N) {
-                            l[k] = srow[member(mode, N, set, k)];
+                            l[k] = srow[mem(set, k)];
                             m = fmaxf(m, l[k]);
                         }
                     float sum = 0.0f;
@@ -236,7 +247,7 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
 #pragma unroll
                         for (int ks = 0; ks < KS; ++ks) {
                             const int k = 4 * ks + kq;
-                            bv[ks] = Vs[member(mode, N, set, k < N ? k : 0) * LDSW + col];
+                            bv[ks] = Vs[mem(set, k < N ? k : 0) * LDSW + col];
                         }
                         const float* p0 = &P[h * PHS + cl * NMAX + kq];
                         const float* p1 = p0 + 16 * NMAX;
@@ -284,7 +295,7 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
                     const int row = mt * 16 + 4 * q + i;
                     if (row < rows) {
                         const int sl = row / N, r = row - sl * N;
-                        const float* xr = &Xs[member(mode, N, s0 + sl, r) * LDSW];
+                        const float* xr = &Xs[mem(s0 + sl, r) * LDSW];
                         PF[row * LDSW + col0] = (acc0[i] + bias0) + xr[col0];
                         PF[row * LDSW + col1] = (acc1[i] + bias1) + xr[col1];
                     }
@@ -726,6 +737,37 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
     else
         RSA_LAUNCH(4);
 #undef RSA_LAUNCH
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_rsa_pool_focal(int32_t B, int32_t N, int32_t A, int32_t heads, int32_t hidden, const float* x,
+                             const float* qkv, const float* w_out, const float* b_out, const int64_t* focal,
+                             float* pooled, void* stream) {
+    if (hidden != HD || B < 0 || N < 1 || N > NMAX || A < 1 || N + A > RMAX) return SWARM_ERR_ARG;
+    if (heads != 1 && heads != 2 && heads != 4) return SWARM_ERR_ARG;
+    if (B == 0) return SWARM_OK;
+    if (!x || !qkv || !w_out || !b_out || !focal || !pooled) return SWARM_ERR_ARG;
+    if ((((uintptr_t)x) | ((uintptr_t)qkv) | ((uintptr_t)pooled)) & 15) return SWARM_ERR_ARG;
+    if (g_cus == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        g_cus = cus;
+    }
+    const int grid = B < g_cus ? B : g_cus;   // one env (its A sets) per iteration
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int mode = SWARM_RSA_FOCAL;
+#define RSA_FOCAL_LAUNCH(NH)                                                                                 \
+    (N == NMAX ? rsa_pool_kernel<NH, NMAX, true><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled, focal, A) \
+               : rsa_pool_kernel<NH, 0, true><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled, focal, A))
+    if (heads == 1)
+        RSA_FOCAL_LAUNCH(1);
+    else if (heads == 2)
+        RSA_FOCAL_LAUNCH(2);
+    else
+        RSA_FOCAL_LAUNCH(4);
+#undef RSA_FOCAL_LAUNCH
     return swarm::record_hip_status();
 }
 

@@ -207,6 +207,40 @@ def test_focal_counterfactuals_at_c4_size(gpu_device):
     torch.testing.assert_close(fused, ref, **TOL)
 
 
+@pytest.mark.parametrize("B,N,A,heads", [(12288, 20, 6, 4), (33, 20, 20, 4), (17, 13, 6, 2), (9, 5, 3, 1),
+                                         (4, 1, 2, 4)])
+def test_focal_shared_sets_match_torch_path(gpu_device, B, N, A, heads):
+    """swarm_rsa_pool_focal (the N joint rows and the A alternative rows of a row embedded
+    once, logits shared by its A sets) against the module's PyTorch path, which embeds and
+    attends the B * A sets separately: C5's 12,288 termination-advantage rows, the largest
+    row block (N + A = 40), runtime set sizes, N = 1."""
+    torch.manual_seed(B + N + A)
+    c = PN.POCACritic(5, A, N, 128, heads, 1, memory_size=128).to(gpu_device).eval()
+    with torch.no_grad():
+        for p in c.parameters():
+            p.add_(torch.randn_like(p) * 0.05)
+        s = torch.randn(B, N, 5, device=gpu_device)
+        ids = torch.randint(0, A, (B, N), device=gpu_device)
+        focal = torch.randint(0, N, (B,), device=gpu_device)
+        mem = (torch.randn(1, B, 64, device=gpu_device), torch.randn(1, B, 64, device=gpu_device))
+        shared = c.focal_discrete_counterfactual_values(s, ids, focal, A, memory=mem)
+        c.use_fused = False
+        ref = c.focal_discrete_counterfactual_values(s, ids, focal, A, memory=mem)
+    torch.testing.assert_close(shared, ref, **TOL)
+
+
+def test_focal_rejects_oversized_row_blocks(gpu_device):
+    from SwarmACB_isaac import _native
+    import ctypes as C
+
+    lib = _native.load()
+    z = torch.zeros(4, device=gpu_device)
+    p = C.c_void_p(z.data_ptr())
+    assert lib.swarm_rsa_pool_focal(1, 20, 21, 4, 128, p, p, p, p, p, p, None) == -1   # N + A > 40
+    assert lib.swarm_rsa_pool_focal(1, 20, 0, 4, 128, p, p, p, p, p, p, None) == -1    # A = 0
+    assert lib.swarm_rsa_pool_focal(1, 20, 6, 4, 128, p, p, p, p, None, p, None) == -1  # no focal ids
+
+
 @pytest.mark.parametrize("memory", [False, True])
 def test_value_and_baselines_shares_rows(gpu_device, fused_calls, memory):
     """The rollout's pair of critic calls on one projection pass (SINGLE_OF_PAIRS +
