@@ -281,40 +281,74 @@ __device__ __forceinline__ float row_norm(const float* a, int D) {
     return fmaxf(sqrtf(s), 1e-8f);
 }
 
-// row partials: diversity sum, temporal sum, attention sum, rows, pairs (one row per thread)
+// row partials: diversity sum, temporal sum, attention sum, rows, pairs. One row per wave: the
+// row's O x D attentions (and the next step's, for the temporal term) are read coalesced into the
+// wave's LDS slot, lane o < O computes option o's inverse norm, lane o * O + p the (o, p) dot
+// product, and the lanes stride the elements for the sums; the wave's butterfly sums are fixed
+// in order, so the partials do not depend on scheduling.
+constexpr int kPartWaves = kPartThreads / 64;
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(kPartThreads) void attn_part_kernel(int B, int L, int O, int D,
                                                                  const float* __restrict__ att,
                                                                  const uint8_t* __restrict__ mask,
                                                                  const float* __restrict__ dones) {
+    __shared__ float rs[kPartWaves][2][kMaxAttnO * kMaxAttnD];
+    __shared__ float inv_s[kPartWaves][kMaxAttnO];
     float v[5] = {0, 0, 0, 0, 0};
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t rows = (int64_t)B * L;
     const int OD = O * D;
-    for (int64_t r = (int64_t)blockIdx.x * kPartThreads + threadIdx.x; r < rows; r += (int64_t)gridDim.x * kPartThreads) {
+    float* x = rs[w][0];
+    float* y = rs[w][1];
+    for (int64_t r = (int64_t)blockIdx.x * kPartWaves + w; r < rows; r += (int64_t)gridDim.x * kPartWaves) {
         const float* a = att + r * OD;
-        const float act = mask[r] ? 1.0f : 0.0f;
-        float inv[kMaxAttnO];
-        for (int o = 0; o < O; ++o) inv[o] = 1.0f / row_norm(a + o * D, D);
-        float div = 0.0f, tot = 0.0f;
-        for (int o = 0; o < O; ++o) {
-            for (int p = 0; p < O; ++p) {
-                if (p == o) continue;
-                float dot = 0.0f;
-                for (int d = 0; d < D; ++d) dot += (a[o * D + d] * inv[o]) * (a[p * D + d] * inv[p]);
-                div += dot;
+        const bool has_next = (int)(r % L) < L - 1;
+        for (int k = lane; k < OD; k += 64) {
+            x[k] = a[k];
+            if (has_next) y[k] = a[OD + k];
+        }
+        wave_fence();
+        if (lane < O) inv_s[w][lane] = 1.0f / row_norm(x + lane * D, D);
+        wave_fence();
+        float div = 0.0f;
+        if (lane < O * O) {
+            const int o = lane / O, p = lane - o * O;
+            if (o != p) {
+                const float io = inv_s[w][o], ip = inv_s[w][p];
+                for (int d = 0; d < D; ++d) div += (x[o * D + d] * io) * (x[p * D + d] * ip);
             }
-            for (int d = 0; d < D; ++d) tot += a[o * D + d];
         }
-        v[0] += div * act;
-        v[2] += tot * act;
-        v[3] += act;
-        const int t = (int)(r % L);
-        if (t < L - 1) {
-            const float pr = (mask[r] && mask[r + 1] && dones[r] < 0.5f) ? 1.0f : 0.0f;
-            float ad = 0.0f;
-            for (int k = 0; k < OD; ++k) ad += fabsf(a[OD + k] - a[k]);
-            v[1] += (ad / (float)OD) * pr;
-            v[4] += pr;
+        float tot = 0.0f, ad = 0.0f;
+        for (int k = lane; k < OD; k += 64) {
+            tot += x[k];
+            if (has_next) ad += fabsf(y[k] - x[k]);
         }
+        div = wave_sum(div);
+        tot = wave_sum(tot);
+        ad = wave_sum(ad);
+        if (lane == 0) {
+            const float act = mask[r] ? 1.0f : 0.0f;
+            v[0] += div * act;
+            v[2] += tot * act;
+            v[3] += act;
+            if (has_next) {
+                const float pr = (mask[r] && mask[r + 1] && dones[r] < 0.5f) ? 1.0f : 0.0f;
+                v[1] += (ad / (float)OD) * pr;
+                v[4] += pr;
+            }
+        }
+        wave_fence();   // the slot is rewritten by the wave's next row
     }
     block_sum_nt<5, kPartThreads>(v);
     if (threadIdx.x == 0) {
@@ -518,7 +552,8 @@ int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, co
     if (B < 1 || L < 1 || O < 2 || O > kMaxAttnO || D < 1 || D > kMaxAttnD || !attentions || !loss_mask || !dones ||
         !out || !used_denoms || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
         return SWARM_ERR_ARG;
-    const int G = part_blocks((int64_t)B * L);
+    const int64_t waves = ((int64_t)B * L + kPartWaves - 1) / kPartWaves;   // one row per wave
+    const int G = (int)(waves < kPartBlocks ? waves : kPartBlocks);
     attn_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask,
                                                                                dones);
     attn_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(G, O, D, row_denom, pair_denom, out,

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--decisions", type=int, default=128)
     ap.add_argument("--envs", type=int, default=256)
+    ap.add_argument("--stack", action="store_true", help="also attribute the glue ops (fill / copy / add / cat) to "
+                    "their Python call sites")
     a = ap.parse_args()
     from SwarmACB_isaac.agents.config import make_env_cfg
     from SwarmACB_isaac.agents.metrics import NullWriter
@@ -49,7 +51,8 @@ def main():
         torch.cuda.synchronize()
         return
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True,
+                 with_stack=a.stack) as prof:
         tr.update()
         torch.cuda.synchronize()
     ka = prof.key_averages()
@@ -58,6 +61,16 @@ def main():
     ks = prof.key_averages(group_by_input_shape=True)
     print(ks.table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=40,
                    max_shapes_column_width=110))
+    if a.stack:
+        glue = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::add", "aten::add_", "aten::cat",
+                "aten::index_put_", "aten::sum", "aten::mul", "aten::clone")
+        rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in glue and e.self_device_time_total > 0]
+        rows.sort(key=lambda e: -e.self_device_time_total)
+        for e in rows[:40]:
+            print(f"{e.self_device_time_total / a.steps:9.1f} us/step  {e.count / a.steps:5.1f} calls/step  {e.key}")
+            for fr in e.stack[:8]:
+                if "SwarmACB_isaac" in fr or "torch/autograd" in fr or "torch/nn" in fr:
+                    print("        ", fr)
     n_kernels = sum(e.count for e in ka if e.device_type == torch.autograd.DeviceType.CUDA)
     print(f"device kernels per optimizer step: {n_kernels / a.steps:.0f}")
 
