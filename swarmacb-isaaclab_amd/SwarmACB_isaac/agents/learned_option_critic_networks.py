@@ -25,6 +25,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.distributions import Categorical, Normal
 
+from . import poca_networks as _PN
 from .poca_networks import LinearEncoder, _linear_layer, _lstm, _mlagents_lstm
 
 LEARNED_OPTION_CRITIC_VERSION = 4
@@ -85,7 +86,12 @@ def _option_heads(head_lists, feats: torch.Tensor) -> list[torch.Tensor]:
     w = torch.cat([torch.cat([hl[o].weight for hl in head_lists], 0) for o in range(O)], 0)    # (O K, H)
     b = torch.stack([torch.cat([hl[o].bias for hl in head_lists], 0) for o in range(O)])       # (O, K)
     lead = feats.shape[:-2]
-    y = torch.nn.functional.linear(feats.reshape(-1, H), w).view(-1, O, O, K)
+    x = feats.reshape(-1, H)
+    if x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= _PN.SPLITK_MIN_ROWS:
+        y = _PN._SplitKLinear.apply(x.contiguous(), w, None)   # the weight gradient over row chunks
+    else:
+        y = torch.nn.functional.linear(x, w)
+    y = y.view(-1, O, O, K)
     y = torch.diagonal(y, dim1=1, dim2=2).transpose(1, 2) + b                                # (rows, O, K)
     return [t.reshape(*lead, O, n) for t, n in zip(torch.split(y, outs, dim=-1), outs)]
 

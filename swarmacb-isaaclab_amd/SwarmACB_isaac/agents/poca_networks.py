@@ -402,9 +402,16 @@ def _lstm_single_step(lstm: nn.LSTM, seq: torch.Tensor, state):
     """lstm(seq, state) for T = 1 (nn.LSTM's gate order i, f, g, o). A keep mask acts only
     between steps, so a single step has none to apply."""
     n, units = seq.shape[0], lstm.hidden_size
-    gates = torch.addmm(torch.nn.functional.linear(seq.reshape(n, -1), lstm.weight_ih_l0,
-                                                   lstm.bias_ih_l0 + lstm.bias_hh_l0),
-                        state[0].reshape(n, units), lstm.weight_hh_l0.t())
+    x, h0 = seq.reshape(n, -1), state[0].reshape(n, units)
+    if seq.is_cuda and torch.is_grad_enabled() and n >= SPLITK_MIN_ROWS:
+        # [x | h0] [W_ih | W_hh]^T + b as ONE product whose weight gradient takes the split-row
+        # reduction (the library's single GEMM for dW_hh over 12,288 rows took 136 us)
+        gates = _SplitKLinear.apply(torch.cat([x, h0], dim=1),
+                                    torch.cat([lstm.weight_ih_l0, lstm.weight_hh_l0], dim=1),
+                                    lstm.bias_ih_l0 + lstm.bias_hh_l0)
+    else:
+        gates = torch.addmm(torch.nn.functional.linear(x, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0),
+                            h0, lstm.weight_hh_l0.t())
     i, f, g, o = gates.chunk(4, dim=1)
     c1 = torch.sigmoid(f) * state[1].reshape(n, units) + torch.sigmoid(i) * torch.tanh(g)
     h1 = torch.sigmoid(o) * torch.tanh(c1)
