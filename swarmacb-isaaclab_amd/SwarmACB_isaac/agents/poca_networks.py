@@ -62,40 +62,47 @@ class _SplitKLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight = ctx.saved_tensors
         dx = dy.mm(weight) if ctx.needs_input_grad[0] else None
-        R = x.shape[0]
-        c = R // SPLITK_CHUNK_ROWS
-        L = R // c
-        main = c * L
-        out_f = dy.shape[1]
-        dyc = dy[:main].view(c, L, out_f)
-        parts = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1]))
-        if SPLITK_NATIVE_SUMS and dy.is_cuda and out_f % 4 == 0 and out_f <= 1024:
-            # the chunk sum of the partial products and the bias gradient (column sums of dy
-            # per slab, then over the slabs) in two launches (swarm_splitk_colsum / _finish)
-            dy = dy.contiguous()
-            lib = _native.load()
-            stream = C.c_void_p(torch.cuda.current_stream(dy.device).cuda_stream)
-            dw = torch.empty(out_f, x.shape[1], dtype=dy.dtype, device=dy.device)
-            db, pb, slabs = None, None, 0
-            if ctx.has_bias:
-                slabs = (R + SPLITK_SLAB_ROWS - 1) // SPLITK_SLAB_ROWS
-                pb = torch.empty(slabs, out_f, dtype=dy.dtype, device=dy.device)
-                db = torch.empty(out_f, dtype=dy.dtype, device=dy.device)
-                _native.check(lib.swarm_splitk_colsum(R, out_f, SPLITK_SLAB_ROWS, _ptr(dy), _ptr(pb), stream),
-                              "swarm_splitk_colsum")
-            _native.check(lib.swarm_splitk_finish(c, dw.numel(), _ptr(parts), _ptr(dw), slabs,
-                                                  out_f if ctx.has_bias else 0, _ptr(pb), _ptr(db), stream),
-                          "swarm_splitk_finish")
-            if main < R:
-                dw.addmm_(dy[main:].t(), x[main:])
-            return dx, dw, db
-        dw = parts.sum(dim=0)
-        db = dyc.sum(dim=1).sum(dim=0) if ctx.has_bias else None
+        dw, db = _split_rows_weight_grad(dy, x, ctx.has_bias)
+        return dx, dw, db
+
+
+def _split_rows_weight_grad(dy, x, has_bias: bool):
+    """(dy^T x, column sums of dy or None) over R >= SPLITK_CHUNK_ROWS rows as _SplitKLinear
+    computes its weight gradient: one batched GEMM over row chunks, then the chunk sums."""
+    R = x.shape[0]
+    c = R // SPLITK_CHUNK_ROWS
+    L = R // c
+    main = c * L
+    out_f = dy.shape[1]
+    dyc = dy[:main].view(c, L, out_f)
+    parts = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1]))
+    if SPLITK_NATIVE_SUMS and dy.is_cuda and out_f % 4 == 0 and out_f <= 1024:
+        # the chunk sum of the partial products and the bias gradient (column sums of dy
+        # per slab, then over the slabs) in two launches (swarm_splitk_colsum / _finish)
+        dy = dy.contiguous()
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(dy.device).cuda_stream)
+        dw = torch.empty(out_f, x.shape[1], dtype=dy.dtype, device=dy.device)
+        db, pb, slabs = None, None, 0
+        if has_bias:
+            slabs = (R + SPLITK_SLAB_ROWS - 1) // SPLITK_SLAB_ROWS
+            pb = torch.empty(slabs, out_f, dtype=dy.dtype, device=dy.device)
+            db = torch.empty(out_f, dtype=dy.dtype, device=dy.device)
+            _native.check(lib.swarm_splitk_colsum(R, out_f, SPLITK_SLAB_ROWS, _ptr(dy), _ptr(pb), stream),
+                          "swarm_splitk_colsum")
+        _native.check(lib.swarm_splitk_finish(c, dw.numel(), _ptr(parts), _ptr(dw), slabs,
+                                              out_f if has_bias else 0, _ptr(pb), _ptr(db), stream),
+                      "swarm_splitk_finish")
         if main < R:
             dw.addmm_(dy[main:].t(), x[main:])
-            if db is not None:
-                db += dy[main:].sum(dim=0)
-        return dx, dw, db
+        return dw, db
+    dw = parts.sum(dim=0)
+    db = dyc.sum(dim=1).sum(dim=0) if has_bias else None
+    if main < R:
+        dw.addmm_(dy[main:].t(), x[main:])
+        if db is not None:
+            db += dy[main:].sum(dim=0)
+    return dw, db
 
 
 class _Linear(nn.Linear):
@@ -233,7 +240,11 @@ class _LSTMSequences(torch.autograd.Function):
                 # W_hh's gradient: dgates^T h_prev' over every (sequence, step) row, one GEMM
                 prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
                 h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
-                dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
+                rows = dxg.numel() // (4 * U)
+                if rows >= SPLITK_MIN_ROWS:   # a 12,288-deep reduction as one GEMM took 134 us
+                    dw = _split_rows_weight_grad(dxg.reshape(rows, 4 * U), h_prev.reshape(rows, U), False)[0]
+                else:
+                    dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
             out += [dxg, dw, dh0, dc0, None]
         return tuple(out)
 
@@ -375,7 +386,13 @@ def lstm_sequences(items):
                 frozen = len(items[i]) > 4 and items[i][4]
                 n, units = seq.shape[0], lstm.hidden_size
                 with torch.no_grad() if frozen else contextlib.nullcontext():
-                    xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0)
+                    bias = lstm.bias_ih_l0 + lstm.bias_hh_l0
+                    rows = seq.shape[0] * seq.shape[1]
+                    if torch.is_grad_enabled() and rows >= SPLITK_MIN_ROWS:
+                        xg = _SplitKLinear.apply(seq.reshape(rows, -1).contiguous(), lstm.weight_ih_l0,
+                                                 bias).view(seq.shape[0], seq.shape[1], -1)
+                    else:
+                        xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, bias)
                     w_hh = lstm.weight_hh_l0.contiguous()
                     h0, c0 = state[0].reshape(n, units).contiguous(), state[1].reshape(n, units).contiguous()
                 if frozen:

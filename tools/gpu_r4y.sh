@@ -3,7 +3,7 @@
 # and the OC2 option heads over >= 8,192 rows: LSTM / OC2 GPU tests, C5 / C4 / C3 optimizer steps.
 set -o pipefail
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/r4y
+OUT=gpurun_out/${TAG:-r4y}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 500 python3 -u -m pytest -q -p no:cacheprovider --timeout 300 --timeout-method thread \
@@ -11,7 +11,7 @@ timeout -k 10 500 python3 -u -m pytest -q -p no:cacheprovider --timeout 300 --ti
   > $OUT/pytest.log 2>&1
 RC=$?; tail -2 $OUT/pytest.log; grep '^FAILED' $OUT/pytest.log | head
 [ $RC -ne 0 ] && exit 3
-for cfg in C5 C4 C3; do
+for cfg in ${CFGS:-C5 C4 C3}; do
   timeout -k 10 300 python3 bench.py --train --config $cfg > $OUT/$cfg.log 2>&1 || { echo "$cfg failed"; tail -5 $OUT/$cfg.log; exit 4; }
   grep '^{' $OUT/$cfg.log | tail -1 > $OUT/bench_train_$cfg.jsonl
   python3 -c "import json; d=json.loads(open('$OUT/bench_train_$cfg.jsonl').read()); print('$cfg ms/opt-step %.3f' % d['ms_per_optimizer_step'])"
