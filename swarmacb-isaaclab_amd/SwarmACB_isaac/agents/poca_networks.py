@@ -37,7 +37,7 @@ _KERNEL_INITS = {
 }
 
 
-SPLITK_MIN_ROWS = 8192     # rows from which a layer's weight gradient is split over row chunks
+SPLITK_MIN_ROWS = 4096     # rows from which a layer's weight gradient is split over row chunks (A/B: profiles/r04/train/splitk_rows_ab.txt)
 SPLITK_CHUNK_ROWS = 1024   # rows per chunk of that split
 SPLITK_SLAB_ROWS = 256     # rows per column-sum slab of its bias gradient
 # False (or SWARM_SPLITK_SUMS=0): the chunk / bias sums run torch's reductions
