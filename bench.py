@@ -21,9 +21,12 @@ from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -160,19 +163,95 @@ def cpu_baseline(budget_s: float, envs: int) -> dict | None:
                       f"E / {cores} envs; value = all-cores rate at E = {envs}"}
 
 
-def load_pmc(envs: int, sub: int) -> dict:
+def lib_sha256(path: str) -> str | None:
+    """sha256 of the step library file (the PMC record is tied to the exact build it measured)."""
+    try:
+        h = hashlib.sha256()
+        with open(path, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 20), b""):
+                h.update(blk)
+        return h.hexdigest()
+    except OSError:
+        return None
+
+
+def load_pmc(envs: int, sub: int, lib_path: str | None, path: str | None = None) -> tuple[dict, str | None]:
     """Per-launch HBM bytes and VALU instruction count of the step kernel from the
-    committed rocprofv3 PMC record (profiles/pmc_traffic.json, tools/pmc.sh), if it
-    was taken on this workload."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    committed rocprofv3 PMC record (profiles/pmc_traffic.json, tools/pmc.sh).
+
+    Returns (record, None) only if the record was taken on this workload AND on the very
+    library this process loaded (its `lib_sha256` stamp equals the loaded file's sha256);
+    otherwise ({}, reason): after any rebuild of the kernels a stale record must not feed the
+    bench line, so `traffic` and the VALU figures are then null with the reason stated."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-    except (OSError, ValueError):
-        return {}
+    except (OSError, ValueError) as e:
+        return {}, f"no PMC record ({type(e).__name__})"
     if d.get("envs") != envs or d.get("substeps") != sub:
-        return {}
-    return d
+        return {}, f"PMC record taken at envs={d.get('envs')} substeps={d.get('substeps')}, not {envs} / {sub}"
+    want = d.get("lib_sha256")
+    have = lib_sha256(lib_path) if lib_path else None
+    if not want:
+        return {}, "PMC record carries no lib_sha256 stamp"
+    if have != want:
+        return {}, f"PMC record measured libswarmstep.so sha256 {want[:12]}..., this process loaded {str(have)[:12]}..."
+    return d, None
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_plan(gpus: int, env: dict) -> tuple[str, str]:
+    """What this process must do for `--gpus N` (no GPU is touched here).
+
+    ("run", "")      : run as one rank (WORLD_SIZE agrees with --gpus, or a single GPU);
+    ("spawn", "")    : --gpus N > 1 and no launcher environment: start N rank processes;
+    ("refuse", why)  : WORLD_SIZE is set and differs from --gpus (a silent 1-GPU number is
+                       the failure this prevents: the line must measure the GPUs it names)."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None and ws != "":
+        if int(ws) != gpus:
+            return "refuse", f"WORLD_SIZE={ws} but --gpus {gpus}: launch {gpus} ranks or pass --gpus {ws}"
+        return "run", ""
+    if gpus == 1:
+        return "run", ""
+    return "spawn", ""
+
+
+def spawn_ranks(gpus: int, argv: list[str], poll_s: float = 0.2, script: str | None = None) -> int:
+    """Start `gpus` fresh rank processes of this script (one per GPU, RANK = LOCAL_RANK = r,
+    WORLD_SIZE = gpus, MASTER_ADDR 127.0.0.1 and a free port) BEFORE this process touches any
+    GPU, wait for them and return the worst exit status. Rank 0 prints the line. If a rank
+    fails, the others (which would wait in a collective forever) are terminated."""
+    port = _free_port()
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(poll_s)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 128 - code)
+                for q in live:
+                    q.terminate()
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def prewarm(seconds: float, eng, E: int, dp: int, dev, out) -> float:
@@ -194,9 +273,68 @@ def prewarm(seconds: float, eng, E: int, dp: int, dev, out) -> float:
     return time.perf_counter() - t0
 
 
+def ranks_table(rank: int, dev, dist) -> list[dict]:
+    """Every rank's (rank, device index, PCI domain:bus:device) from the live process group, so
+    the line shows which physical GPUs ran (one entry per rank)."""
+    p = torch.cuda.get_device_properties(dev)
+    mine = [rank, dev.index, int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id)]
+    if dist is None:
+        rows = [mine]
+    else:
+        t = torch.tensor(mine, dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(out, t)
+        rows = [o.tolist() for o in out]
+    return [{"rank": r, "device": d, "pci": f"{a:04x}:{b:02x}:{c:02x}"} for r, d, a, b, c in rows]
+
+
+def valu_roofline(pmc: dict, pmc_why: str | None, avg_kernel_s: float, hbm_achieved: float, traffic, E: int,
+                  dp: int, bytes_per_launch: float, lib_sha: str | None) -> dict:
+    """The step kernel's roofline line: the binding roof is VALU issue
+    (~80 op/B against a ~20 op/B ridge), so `bound` is "valu" with the measured SQ_INSTS_VALU
+    x 64 lane-ops / kernel time against 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz; HBM
+    (algorithmic bytes / kernel time, and the PMC traffic) is the secondary roof. The VALU
+    count and the traffic come from the PMC record only when it was taken on the loaded
+    library (load_pmc); otherwise they are null and `pmc_status` says why."""
+    valu_insts = pmc.get("valu_insts_per_launch")
+    lane_ops = valu_insts * 64.0 if valu_insts else None
+    achieved = lane_ops / avg_kernel_s / 1e12 if lane_ops else None
+    return {
+        "bound": "valu",
+        "achieved": achieved,
+        "peak": VALU_PEAK_LANE_OPS / 1e12,
+        "unit": "T lane-ops/s",
+        "frac": (lane_ops / avg_kernel_s / VALU_PEAK_LANE_OPS) if lane_ops else None,
+        "traffic": traffic,
+        "valu_insts_per_launch": valu_insts,
+        "valu_busy": pmc.get("valu_busy"),
+        "sq_wait_any_frac": pmc.get("sq_wait_any_frac"),
+        "pmc_status": "ok" if pmc_why is None else pmc_why,
+        "pmc_source": "profiles/pmc_traffic.json (rocprofv3 --pmc passes of this workload, tools/pmc.sh), "
+                      "stamped with the sha256 of the libswarmstep.so it measured",
+        "lib_sha256": lib_sha,
+        "kernel": "step_kernel<HOMING,ISAAC,continuous,N=20,layout 103>",
+        "kernel_avg_us": avg_kernel_s * 1e6,
+        "secondary": {
+            "bound": "hbm",
+            "achieved": hbm_achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": hbm_achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "traffic_per_agent_step": (traffic / (E * N_AGENTS * dp)) if traffic else None,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+    }
+
+
 def main():
     args = parse()
     if args.rollout or args.critic or args.collect or args.train:
+        if args.gpus != 1 and os.environ.get("WORLD_SIZE") is None:
+            print("bench.py: --rollout/--critic/--collect/--train are single-GPU measurements; "
+                  "pass --gpus 1 (or launch ranks yourself)", file=sys.stderr, flush=True)
+            sys.exit(2)
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         sys.argv = [sys.argv[0]] + args.rest
         if args.train:
@@ -216,13 +354,26 @@ def main():
 
             bench_critic.main()
         return
+    # --gpus N decides the world: spawn N ranks here (before any torch.cuda call), run as one
+    # rank of a launcher that agrees, or refuse a mismatch
+    plan, why = rank_plan(args.gpus, os.environ)
+    if plan == "refuse":
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    # one process per GPU; (rank % visible devices) only matters when rehearsing
-    # several ranks on one device (with --dist-backend gloo: RCCL refuses that)
-    local = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > 1 and local >= ndev:
+        print(f"bench.py: rank {rank} has LOCAL_RANK {local} but only {ndev} GPUs are visible "
+              f"(RCCL needs one GPU per rank)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    # (rank % visible devices) only matters when rehearsing several ranks on one device
+    # (--dist-backend gloo: RCCL refuses that)
+    local = local % max(1, ndev)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -287,6 +438,7 @@ def main():
     torch.cuda.synchronize(dev)
     if gate is not None:
         flag.value = 0
+        C.c_uint32.from_address(gate.value + 4).value = 0
         _native.check(eng.lib.swarm_gate_wait(gate, 10_000_000, C.c_void_p(stream.cuda_stream)), "swarm_gate_wait")
     ev0.record(stream)
     if graph is not None:
@@ -302,32 +454,40 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gate_timed_out = False
     if gate is not None:
+        # word 1 of the gate buffer: set by gate_kernel when it released on its timeout instead
+        # of the host's flag (the host enqueue blocked; the timed launches then started before
+        # t0 and the wall clock would miss them)
+        gate_timed_out = C.c_uint32.from_address(gate.value + 4).value != 0
         _native.check(eng.lib.swarm_gate_free(gate), "swarm_gate_free")
-    avg_kernel_s = ev0.elapsed_time(ev1) / n_dec / 1e3
+    region_s = ev0.elapsed_time(ev1) / 1e3
+    avg_kernel_s = region_s / n_dec
+    if gate_timed_out or elapsed < 0.98 * region_s:
+        print(f"bench.py: rank {rank}: invalid timed region (gate timed out: {gate_timed_out}; wall "
+              f"{elapsed * 1e3:.3f} ms vs GPU events {region_s * 1e3:.3f} ms): rerun with fewer --steps",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
     elapsed = max_over_ranks(elapsed, dev)
-    total_agent_steps = world * E * N_AGENTS * steps
+    ranks_seen = ranks_table(rank, dev, dist)
+    world_live = dist.get_world_size() if dist is not None else 1
+    total_agent_steps = world_live * E * N_AGENTS * steps
     value = total_agent_steps / elapsed
 
     if rank == 0:
         bytes_per_launch = ALGO_BYTES_PER_AGENT_STEP * E * N_AGENTS * dp
         achieved = bytes_per_launch / avg_kernel_s / 1e9
-        pmc = load_pmc(E, dp)
+        lib_path = getattr(eng.lib, "_name", None)
+        pmc, pmc_why = load_pmc(E, dp, lib_path)
         traffic = pmc.get("hbm_bytes_per_launch")
-        valu = None
-        if pmc.get("valu_insts_per_launch"):
-            # VALU issue roof: 256 CUs x 4 SIMD32 x 32 lanes/clk x 2.4 GHz (a wave64 VALU op = 64 lane-ops)
-            lane_ops = pmc["valu_insts_per_launch"] * 64.0
-            peak = VALU_PEAK_LANE_OPS
-            valu = {"achieved": lane_ops / avg_kernel_s / 1e12, "peak": peak / 1e12, "unit": "T lane-ops/s",
-                    "frac": lane_ops / avg_kernel_s / peak,
-                    "valu_insts_per_launch": pmc["valu_insts_per_launch"],
-                    "valu_insts_source": "profiles/pmc_traffic.json (SQ_INSTS_VALU pass); not measured in this process"}
+        roofline = valu_roofline(pmc, pmc_why, avg_kernel_s, achieved, traffic, E, dp, bytes_per_launch,
+                                 lib_sha256(lib_path) if lib_path else None)
         line = {
             "metric": METRIC,
             "value": value,
             "unit": "agent-steps/s",
-            "n_gpus": world,
+            "n_gpus": world_live,
+            "ranks_seen": ranks_seen,
             "steps": steps,
             "warmup": n_warm * dp,
             "prewarm_s": prewarm_s,
@@ -351,22 +511,8 @@ def main():
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of "
-                                  "this workload, tools/pmc.sh); not measured in this process" if traffic else None,
-                "traffic_per_agent_step": (traffic / (E * N_AGENTS * dp)) if traffic else None,
-                "valu": valu,
-                "kernel": "step_kernel<HOMING,ISAAC,continuous,N=20,W>",
-                "kernel_avg_us": avg_kernel_s * 1e6,
-                "algorithmic_bytes_per_launch": bytes_per_launch,
-            },
-            "cpu_baseline": cpu_baseline(args.cpu_seconds if world == 1 else 0.0, E),
+            "roofline": roofline,
+            "cpu_baseline": cpu_baseline(args.cpu_seconds if world_live == 1 else 0.0, E),
         }
         print(json.dumps(line), flush=True)
     eng.close()

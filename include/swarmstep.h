@@ -167,9 +167,11 @@ int64_t swarm_tick(const swarm_handle_t* h);
 int64_t swarm_last_timeouts(const swarm_handle_t* h);
 
 /* Measurement helpers (no reference counterpart; bench.py): a stream gate. swarm_gate_alloc
- * returns a host-coherent flag word (0); swarm_gate_wait enqueues a one-wave kernel on `stream`
- * that returns once the host has set *flag nonzero, or after timeout_us (at most 60 s), so the
- * launches enqueued behind it run back to back from the release on. swarm_gate_free releases it. */
+ * returns a host-coherent buffer of two words, both 0: word 0 is the release flag, word 1 is set
+ * to 1 by the gate kernel when it released on its time limit instead of the host's flag.
+ * swarm_gate_wait enqueues a one-wave kernel on `stream` that waits until word 0 is non-zero (or
+ * `timeout_us` passes), so launches enqueued behind it run back to back from the release on.
+ * swarm_gate_free releases it. */
 int32_t swarm_gate_alloc(uint32_t** flag);
 int32_t swarm_gate_free(uint32_t* flag);
 int32_t swarm_gate_wait(const uint32_t* flag, int64_t timeout_us, void* stream);

@@ -181,10 +181,13 @@ int32_t swarm_categorical_terms_backward(int64_t M, int32_t K, const float* logi
 /* The learned-option (OC2) update's termination, option-selection and attention terms (agents/
  * learned_option_critic_trainer.py:1050-1093, 1140-1169, 1282-1322, 956-997; csrc/swarm_oc2terms.hip
  * states every formula). Each forward writes device scalars (the attention and option forwards
- * reduce over many workgroups into a library buffer, then add the workgroups' sums in a fixed order:
- * one stream at a time; denominators: the given device scalar, or the local active count clamped to
- * >= 1; the one used is returned for the backward); each backward is elementwise and reads its
- * incoming gradients from a device array.
+ * reduce over many workgroups into the caller's `partials` workspace of SWARM_OC2_PARTIALS_FLOATS
+ * floats, then add the workgroups' sums in a fixed order: give every concurrent call its own;
+ * denominators: the given device scalar, or the local active count clamped to >= 1; the one used is
+ * returned for the backward); each backward is elementwise and reads its incoming gradients from a
+ * device array. `bad_inputs` (a device int32 the caller zeroes and reads, or NULL) gets bit 2 (an
+ * option index outside [0, O): Categorical.log_prob raises on it) or bit 4 (a non-finite mean or a
+ * non-finite / non-positive std: Normal(loc, scale)'s validation raises on it) ORed in.
  *   termination: out[8] = loss, prior loss, entropy, mean beta, mean advantage, mean signal, low /
  *     high saturation over M rows of logits / advantages / term_mask (f32); grads[3] = d/d out[0..2];
  *   option terms (epsilon-greedy manager, forward only): out[5] = sum log_prob, option entropy,
@@ -202,20 +205,24 @@ int32_t swarm_oc2_termination_terms_backward(int64_t M, const float* logits, con
                                              const float* term_mask, const float* used_denom, float penalty,
                                              float prior_probability, const float* grads, float* d_logits,
                                              void* stream);
+#define SWARM_OC2_PARTIALS_FLOATS (2048 * 24)
 int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values, const int64_t* options,
                                const uint8_t* loss_mask, const uint8_t* boundary, const float* boundary_denom,
-                               float low, float greedy_add, float log_num_options, float* out, void* stream);
+                               float low, float greedy_add, float log_num_options, float* out, float* partials,
+                               int32_t* bad_inputs, void* stream);
 int32_t swarm_oc2_action_terms(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
                                const float* ref_means, const float* ref_stds, const float* actions,
                                const float* old_log_probs, const uint8_t* loss_mask, const float* row_denom,
-                               float* log_probs, float* ref_log_probs, float* out, float* used_denom, void* stream);
+                               float* log_probs, float* ref_log_probs, float* out, float* used_denom,
+                               int32_t* bad_inputs, void* stream);
 int32_t swarm_oc2_action_terms_backward(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
                                         const float* actions, const uint8_t* loss_mask, const float* used_denom,
                                         const float* grad_log_probs, const float* grad_out, float* d_means,
                                         float* d_stds, void* stream);
 int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
                                   const uint8_t* loss_mask, const float* dones, const float* row_denom,
-                                  const float* pair_denom, float* out, float* used_denoms, void* stream);
+                                  const float* pair_denom, float* out, float* used_denoms, float* partials,
+                                  void* stream);
 int32_t swarm_oc2_attention_terms_backward(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
                                            const uint8_t* loss_mask, const float* dones, const float* used_denoms,
                                            const float* grads, float* d_attentions, void* stream);

@@ -81,6 +81,7 @@ TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa
                  "swarm_oc2_attention_terms_backward", "swarm_oc2_action_terms", "swarm_oc2_action_terms_backward"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
+OC2_PARTIALS_FLOATS = 2048 * 24   # SWARM_OC2_PARTIALS_FLOATS (include/swarmtrain.h)
 
 
 class LstmSeqFwd(C.Structure):
@@ -219,13 +220,14 @@ def load() -> C.CDLL:
     lib.swarm_oc2_termination_terms_backward.restype = i32
     lib.swarm_oc2_termination_terms_backward.argtypes = [i64, vp, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp]
     lib.swarm_oc2_option_terms.restype = i32
-    lib.swarm_oc2_option_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, vp, vp]
+    lib.swarm_oc2_option_terms.argtypes = [i64, i32, vp, vp, vp, vp, vp, C.c_float, C.c_float, C.c_float, vp, vp, vp,
+                                           vp]
     lib.swarm_oc2_action_terms.restype = i32
-    lib.swarm_oc2_action_terms.argtypes = [i64, i32, i32] + [vp] * 12
+    lib.swarm_oc2_action_terms.argtypes = [i64, i32, i32] + [vp] * 13
     lib.swarm_oc2_action_terms_backward.restype = i32
     lib.swarm_oc2_action_terms_backward.argtypes = [i64, i32, i32] + [vp] * 10
     lib.swarm_oc2_attention_terms.restype = i32
-    lib.swarm_oc2_attention_terms.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.swarm_oc2_attention_terms.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_oc2_attention_terms_backward.restype = i32
     lib.swarm_oc2_attention_terms_backward.argtypes = [i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_categorical_terms_backward.restype = i32

@@ -99,8 +99,23 @@ class RolloutStorage:
             self.slot_of_row[r] = torch.where(start, slot, -1).to(torch.int32)
             self._n_slots += start
             self._slot = slot
+            if r % self.OVERFLOW_CHECK_ROWS == self.OVERFLOW_CHECK_ROWS - 1:
+                self.check_start_slots()
         self._slot_row = t
         return self._slot
+
+    # rows between two host reads of the slot-overflow flags (one sync per 32 decisions)
+    OVERFLOW_CHECK_ROWS = 32
+
+    def check_start_slots(self):
+        """Fail fast (one host read) if an env claimed more chunk starts than its slot budget:
+        the budget assumes episodes that end at the time limit (every mission's _get_dones,
+        directional_gate_env.py:1200-1209); an env whose episodes end earlier would otherwise
+        only be reported by _sequence_batches after the whole rollout was collected."""
+        if self.compact_starts and bool(self._overflow.any()):
+            raise RuntimeError(f"chunk-start storage: an env needs more than its {self.start_slots} chunk-start "
+                               f"slots (episodes shorter than the {self.horizon}-row budget assumes?); build the "
+                               f"buffer without episode_decisions to keep the plain (T, E, ...) layout")
 
     def put_start(self, attr: str, t: int, value: torch.Tensor):
         """buffer.<attr>[t] = value for a START_FIELDS tensor (either layout)."""

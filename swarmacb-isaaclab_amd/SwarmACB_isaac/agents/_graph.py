@@ -33,8 +33,10 @@ ENABLED = os.environ.get("SWARM_GRAPHS", "1") != "0"
 # On by default since round 4: on MI355X a world-1 RCCL group running every collective of the
 # multi-rank update eagerly, then captured and replayed, gives the eager update bit for bit
 # (tests/test_gpu_rccl_graph.py; two ranks need two GPUs, which one process never gets here).
-# Every rank reports whether its steps were graphed (Trainer.step_path), and a capture that
-# fails falls back to eager steps, which issue the same collectives in the same order.
+# Every rank reports whether its steps were graphed (Trainer.step_path). Whether a capture
+# succeeded is agreed on by all ranks before the first replay (one MIN all-reduce of a flag,
+# outside the graph): if any rank could not capture, every rank drops its graph and runs its
+# steps eagerly, so no rank replays a captured collective that another rank issues eagerly.
 DIST_ENABLED = os.environ.get("SWARM_GRAPHS_DIST", "1") != "0"
 
 
@@ -47,6 +49,19 @@ def make_capturable(optimizers, device: torch.device):
             s = st.get("step")
             if isinstance(s, torch.Tensor) and s.device != device:
                 st["step"] = s.to(device=device, dtype=torch.float32)
+
+
+def all_ranks_agree(ok: bool) -> bool:
+    """True iff `ok` holds on every rank of the default process group (one MIN all-reduce of a
+    flag, issued eagerly on the current stream); `ok` itself without a multi-rank group."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() < 2:
+        return ok
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
 
 
 class GraphedStep:
@@ -102,12 +117,19 @@ class GraphedStep:
         self.static = {k: v.clone() for k, v in batch.items()}
         self.sig = sig
         self.graph = torch.cuda.CUDAGraph()
+        ok = True
         try:
             with torch.cuda.graph(self.graph):
                 self.out = self.fn(self.static)
         except RuntimeError as e:   # torch.AcceleratorError derives from RuntimeError
             where = "".join(traceback.format_exception(e)[-8:-1])
             warnings.warn(f"optimizer step not capturable, running eagerly: {e}\n{where}")
+            ok = False
+        # every rank takes the same path (captured collectives replayed on one rank and eager
+        # ones on another would pair up wrongly and hang)
+        if not all_ranks_agree(ok):
+            if ok:
+                warnings.warn("another rank could not capture its optimizer step: running eagerly like it")
             self.failed = True
             self.reset(self.key)
             torch.cuda.synchronize()

@@ -212,24 +212,42 @@ _BAD_ACTIONS: dict = {}
 
 
 def _bad_action_flag(device) -> torch.Tensor:
-    """The device int32 swarm_categorical_terms sets when an action is outside [0, K) (one per
-    device, allocated before any graph capture by the first eager step)."""
+    """The device int32 the fused policy terms OR their input-check bits into (one per device,
+    allocated before any graph capture by the first eager step): 1 = a categorical action outside
+    [0, K) (swarm_categorical_terms), 2 = an OC2 option outside [0, O) (swarm_oc2_option_terms),
+    4 = a non-finite mean or non-finite / non-positive std of the OC2 wheel policy
+    (swarm_oc2_action_terms)."""
     key = str(device)
     if key not in _BAD_ACTIONS:
         _BAD_ACTIONS[key] = torch.zeros(1, dtype=torch.int32, device=device)
     return _BAD_ACTIONS[key]
 
 
-def check_categorical_actions(device) -> None:
-    """Raise if a categorical term of this device saw an action outside [0, K) since the last
-    check (torch's Categorical.log_prob / gather raises on such an index; the fused kernel flags
-    it instead of returning a silent NaN). One host read, called once per update."""
+def check_policy_inputs(device) -> None:
+    """Raise if a fused policy term of this device saw an input the reference's torch.distributions
+    would reject since the last check: Categorical.log_prob / gather raise on an index outside
+    [0, K), Normal(loc, scale) (built with validation on, learned_option_critic_networks.py) on a
+    NaN / infinite / non-positive scale. The kernels flag instead of returning a silent NaN; one
+    host read, called once per update."""
     flag = _BAD_ACTIONS.get(str(device))
-    if flag is not None and int(flag.item()):
-        flag.zero_()
+    if flag is None:
+        return
+    bits = int(flag.item())
+    if not bits:
+        return
+    flag.zero_()
+    if bits & 1:
         raise IndexError("categorical policy terms: an action / option index outside [0, K) reached the "
                          "update (e.g. the -1 'fresh option' sentinel); torch.distributions.Categorical "
                          "would raise on it too")
+    if bits & 2:
+        raise IndexError("OC2 option terms: an option index outside [0, num_options) reached the update; "
+                         "torch.distributions.Categorical would raise on it too")
+    raise ValueError("OC2 action terms: a non-finite mean or a non-finite / non-positive standard deviation "
+                     "reached the update; torch.distributions.Normal's argument validation would raise on it too")
+
+
+check_categorical_actions = check_policy_inputs
 
 
 def categorical_terms(logits, actions, mask=None, denom=None):

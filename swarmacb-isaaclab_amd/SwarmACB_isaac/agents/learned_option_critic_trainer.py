@@ -39,7 +39,8 @@ import torch.optim as optim
 from torch.distributions import Bernoulli
 
 from .. import _native
-from ._trainer import PolynomialDecay, TrainerBase, _fused_policy_loss, stack_obs, trust_region_value_loss
+from ._trainer import (PolynomialDecay, TrainerBase, _bad_action_flag, _fused_policy_loss, check_policy_inputs,
+                       stack_obs, trust_region_value_loss)
 from .config import PAPER_PARITY_VERSION, LearnedOptionCriticConfig
 from .distributed import TrainerComm
 from .learned_option_critic_buffer import LearnedOptionRolloutBuffer
@@ -144,9 +145,10 @@ class _AttentionTerms(torch.autograd.Function):
         B, L, O, D = a.shape
         out = torch.empty(3, dtype=a.dtype, device=a.device)
         used = torch.empty(2, dtype=a.dtype, device=a.device)
+        part = torch.empty(_native.OC2_PARTIALS_FLOATS, dtype=torch.float32, device=a.device)
         _native.check(_native.load().swarm_oc2_attention_terms(
             B, L, O, D, _vp(a), _vp(mask_u8), _vp(dones), _vp(d_rows), _vp(d_pairs), _vp(out), _vp(used),
-            _stream(a)), "swarm_oc2_attention_terms")
+            _vp(part), _stream(a)), "swarm_oc2_attention_terms")
         ctx.save_for_backward(a, mask_u8, dones, used)
         return out
 
@@ -178,8 +180,8 @@ class _ActionTerms(torch.autograd.Function):
         used = torch.empty((), dtype=mu.dtype, device=mu.device)
         _native.check(_native.load().swarm_oc2_action_terms(
             M, A, int(squashed), _vp(mu), _vp(sg), _vp(ref_means), _vp(ref_stds), _vp(actions), _vp(old_lp),
-            _vp(mask_u8), _vp(row_denom), _vp(lp), _vp(lp_r), _vp(out), _vp(used), _stream(mu)),
-            "swarm_oc2_action_terms")
+            _vp(mask_u8), _vp(row_denom), _vp(lp), _vp(lp_r), _vp(out), _vp(used), _vp(_bad_action_flag(mu.device)),
+            _stream(mu)), "swarm_oc2_action_terms")
         ctx.save_for_backward(mu, sg, actions, mask_u8, used)
         ctx.squashed = bool(squashed)
         ctx.mark_non_differentiable(lp_r)
@@ -259,11 +261,13 @@ def fused_option_terms(actor, option_values, options, loss_mask, boundary, epsil
     q = option_values.detach().reshape(-1, O).contiguous()
     M = q.shape[0]
     out = torch.empty(5, dtype=torch.float32, device=q.device)
+    part = torch.empty(_native.OC2_PARTIALS_FLOATS, dtype=torch.float32, device=q.device)
     _native.check(_native.load().swarm_oc2_option_terms(
         M, O, _vp(q), _vp(options.reshape(-1).long().contiguous()),
         _vp(loss_mask.reshape(-1).to(torch.bool).contiguous().view(torch.uint8)),
         _vp(boundary.reshape(-1).to(torch.bool).contiguous().view(torch.uint8)), _vp(d),
-        float(epsilon) / O, 1.0 - float(epsilon), math.log(O), _vp(out), _stream(q)), "swarm_oc2_option_terms")
+        float(epsilon) / O, 1.0 - float(epsilon), math.log(O), _vp(out), _vp(part),
+        _vp(_bad_action_flag(q.device)), _stream(q)), "swarm_oc2_option_terms")
     return tuple(out[k] for k in range(5))
 
 
@@ -874,11 +878,17 @@ class LearnedOptionCriticTrainer(TrainerBase):
                 step(batch, key)
         G = self._g
         host = torch.cat([G["nb"].reshape(1), G["actor_updates"].reshape(1), G["init_kl"].reshape(1), G["max_kl"],
-                          G["stopped"].double().reshape(1), G["bad"].double()]).tolist()
+                          G["stopped"].double().reshape(1), G["bad"].double(),
+                          _bad_action_flag(self.device).double()]).tolist()
         num_batches, actor_updates, initial_policy_kl = int(host[0]), int(host[1]), host[2]
         max_policy_kl, max_action_kl, max_option_kl = host[3:6]
         actor_early_stopped = bool(host[6])
         bad = host[7:11]
+        if host[11]:
+            try:
+                check_policy_inputs(self.device)      # the option / Normal checks of the fused terms
+            except (IndexError, ValueError) as e:
+                fail(e)
         if num_batches and initial_policy_kl > 1e-6:
             fail(RuntimeError(f"OC2 update-start policy does not match its frozen reference "
                               f"(KL={initial_policy_kl:.6g})."))
@@ -961,6 +971,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         if actor_updates == 0:
             raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
                                "should guarantee at least one safe policy minibatch.")
+        check_policy_inputs(self.device)
         modules = (("actor", self.actor), ("team_critic", self.team_critic), ("action_critic", self.action_critic),
                    ("option_critic", self.option_critic))
         named = [(f"{m}.{n}", p) for m, mod in modules for n, p in mod.named_parameters()]

@@ -60,13 +60,18 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kBwdThreads = 256;
 
 // Multi-block forwards (attention, option terms): block b writes its K partial sums to row b of
-// this buffer, then one finalising workgroup adds the rows in block order (a fixed order, so the
-// result does not depend on scheduling: graph replays equal eager runs bit for bit). One stream
-// at a time uses it (the trainer's update stream).
+// the caller's `partials` workspace (SWARM_OC2_PARTIALS_FLOATS floats, one per call: concurrent
+// calls on other streams or graphs never share it), then one finalising workgroup adds the rows
+// in block order (a fixed order, so the result does not depend on scheduling: graph replays
+// equal eager runs bit for bit).
 constexpr int kPartBlocks = 2048;
 constexpr int kPartK = 24;
-__device__ float g_part[kPartBlocks * kPartK];
+static_assert(kPartBlocks * kPartK == SWARM_OC2_PARTIALS_FLOATS, "workspace size of include/swarmtrain.h");
 constexpr int kPartThreads = 256;
+
+// bits of the caller's input-check flag (include/swarmtrain.h)
+constexpr int32_t kBadOption = 2;   // an option index outside [0, O)
+constexpr int32_t kBadStd = 4;      // a non-finite or non-positive standard deviation
 
 // block-wide sum of K per-thread partials over an NT-thread block; the result is valid in thread 0
 template <int K, int NT>
@@ -99,7 +104,7 @@ __device__ __forceinline__ void block_sum_nt(float (&v)[K]) {
 // values on both lanes of a pair), so the order is fixed and independent of scheduling. (One
 // sequential thread per column took 134 us over the attention forward's 512 blocks.)
 template <int K>
-__device__ __forceinline__ void part_sums(int G, float* sums) {
+__device__ __forceinline__ void part_sums(const float* __restrict__ g_part, int G, float* sums) {
     __shared__ float col[K];
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -239,14 +244,19 @@ __global__ __launch_bounds__(kPartThreads) void option_part_kernel(int64_t M, in
                                                                    const int64_t* __restrict__ options,
                                                                    const uint8_t* __restrict__ mask,
                                                                    const uint8_t* __restrict__ boundary, float low,
-                                                                   float greedy_add) {
+                                                                   float greedy_add, float* __restrict__ g_part,
+                                                                   int32_t* __restrict__ bad) {
     float v[4 + kMaxOptions];
 #pragma unroll
     for (int k = 0; k < 4 + kMaxOptions; ++k) v[k] = 0.0f;
     float lo, hi, llo, lhi;
     option_probs(O, low, greedy_add, lo, hi, llo, lhi);
-    for (int64_t m = (int64_t)blockIdx.x * kPartThreads + threadIdx.x; m < M; m += (int64_t)gridDim.x * kPartThreads)
-        option_row(O, q + m * O, options[m], boundary[m] ? 1.0f : 0.0f, mask[m] ? 1.0f : 0.0f, lo, hi, llo, lhi, v);
+    for (int64_t m = (int64_t)blockIdx.x * kPartThreads + threadIdx.x; m < M; m += (int64_t)gridDim.x * kPartThreads) {
+        const int64_t opt = options[m];
+        // Categorical.log_prob raises on such an index (its value check); flag it for the host
+        if ((opt < 0 || opt >= O) && bad) atomicOr(bad, kBadOption);
+        option_row(O, q + m * O, opt, boundary[m] ? 1.0f : 0.0f, mask[m] ? 1.0f : 0.0f, lo, hi, llo, lhi, v);
+    }
     block_sum_nt<4 + kMaxOptions, kPartThreads>(v);
     if (threadIdx.x == 0) {
 #pragma unroll
@@ -254,10 +264,10 @@ __global__ __launch_bounds__(kPartThreads) void option_part_kernel(int64_t M, in
     }
 }
 
-__global__ __launch_bounds__(64) void option_fin_kernel(int G, int O, const float* denom_b, float log_o,
-                                                        float* __restrict__ out) {
+__global__ __launch_bounds__(64) void option_fin_kernel(const float* __restrict__ g_part, int G, int O,
+                                                        const float* denom_b, float log_o, float* __restrict__ out) {
     __shared__ float v[4 + kMaxOptions];
-    part_sums<4 + kMaxOptions>(G, v);
+    part_sums<4 + kMaxOptions>(g_part, G, v);
     if (threadIdx.x == 0) {
         const float nb = denom_b ? *denom_b : fmaxf(v[2], 1.0f);
         const float nm = fmaxf(v[3], 1.0f);
@@ -307,7 +317,8 @@ __device__ __forceinline__ void wave_fence() {
 __global__ __launch_bounds__(kPartThreads) void attn_part_kernel(int B, int L, int O, int D,
                                                                  const float* __restrict__ att,
                                                                  const uint8_t* __restrict__ mask,
-                                                                 const float* __restrict__ dones) {
+                                                                 const float* __restrict__ dones,
+                                                                 float* __restrict__ g_part) {
     __shared__ float rs[kPartWaves][2][kMaxAttnO * kMaxAttnD];
     __shared__ float inv_s[kPartWaves][kMaxAttnO];
     float v[5] = {0, 0, 0, 0, 0};
@@ -362,10 +373,11 @@ __global__ __launch_bounds__(kPartThreads) void attn_part_kernel(int B, int L, i
     }
 }
 
-__global__ __launch_bounds__(64) void attn_fin_kernel(int G, int O, int D, const float* d_rows, const float* d_pairs,
+__global__ __launch_bounds__(64) void attn_fin_kernel(const float* __restrict__ g_part, int G, int O, int D,
+                                                      const float* d_rows, const float* d_pairs,
                                                       float* __restrict__ out, float* __restrict__ used) {
     __shared__ float v[5];
-    part_sums<5>(G, v);
+    part_sums<5>(g_part, G, v);
     if (threadIdx.x == 0) {
         const float nr = d_rows ? *d_rows : fmaxf(v[3], 1.0f);
         const float np = d_pairs ? *d_pairs : fmaxf(v[4], 1.0f);
@@ -461,11 +473,16 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(int64_t M, int A, 
                                                               const uint8_t* __restrict__ mask,
                                                               const float* row_denom, float* __restrict__ lp,
                                                               float* __restrict__ lp_r, float* __restrict__ out,
-                                                              float* __restrict__ used) {
+                                                              float* __restrict__ used, int32_t* __restrict__ bad) {
     float v[4] = {0, 0, 0, 0};   // kl sum, behaviour sum, entropy sum, mask count
     const int64_t n = M * A;
     for (int64_t i = threadIdx.x; i < n; i += kThreads) {
         const int64_t m = i / A;
+        // Normal(loc, scale)'s argument validation rejects a NaN / infinite or non-positive scale
+        // (the reference builds it with validation on); flag it for the host
+        const bool ok = isfinite(sg[i]) && sg[i] > 0.0f && isfinite(sg_r[i]) && sg_r[i] > 0.0f &&
+                        isfinite(mu[i]) && isfinite(mu_r[i]);
+        if (!ok && bad) atomicOr(bad, kBadStd);
         float ld;
         const float u = pre_tanh_of(x[i], squash != 0, ld);
         const float a = normal_logp(u, mu[i], sg[i]) - ld;
@@ -541,27 +558,31 @@ int32_t swarm_oc2_termination_terms_backward(int64_t M, const float* logits, con
 
 int32_t swarm_oc2_option_terms(int64_t M, int32_t O, const float* option_values, const int64_t* options,
                                const uint8_t* loss_mask, const uint8_t* boundary, const float* boundary_denom,
-                               float low, float greedy_add, float log_num_options, float* out, void* stream) {
-    if (M < 1 || O < 1 || O > kMaxOptions || !option_values || !options || !loss_mask || !boundary || !out)
+                               float low, float greedy_add, float log_num_options, float* out, float* partials,
+                               int32_t* bad_inputs, void* stream) {
+    if (M < 1 || O < 1 || O > kMaxOptions || !option_values || !options || !loss_mask || !boundary || !out ||
+        !partials)
         return SWARM_ERR_ARG;
     const int G = part_blocks(M);
-    option_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(M, O, option_values, options,
-                                                                                 loss_mask, boundary, low, greedy_add);
-    option_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(G, O, boundary_denom, log_num_options, out);
+    option_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(
+        M, O, option_values, options, loss_mask, boundary, low, greedy_add, partials, bad_inputs);
+    option_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(partials, G, O, boundary_denom,
+                                                                      log_num_options, out);
     return status();
 }
 
 int32_t swarm_oc2_attention_terms(int32_t B, int32_t L, int32_t O, int32_t D, const float* attentions,
                                   const uint8_t* loss_mask, const float* dones, const float* row_denom,
-                                  const float* pair_denom, float* out, float* used_denoms, void* stream) {
+                                  const float* pair_denom, float* out, float* used_denoms, float* partials,
+                                  void* stream) {
     if (B < 1 || L < 1 || O < 2 || O > kMaxAttnO || D < 1 || D > kMaxAttnD || !attentions || !loss_mask || !dones ||
-        !out || !used_denoms || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
+        !out || !used_denoms || !partials || (int64_t)B * L * O * D >= ((int64_t)1 << 31))
         return SWARM_ERR_ARG;
     const int64_t waves = ((int64_t)B * L + kPartWaves - 1) / kPartWaves;   // one row per wave
     const int G = (int)(waves < kPartBlocks ? waves : kPartBlocks);
     attn_part_kernel<<<G, kPartThreads, 0, static_cast<hipStream_t>(stream)>>>(B, L, O, D, attentions, loss_mask,
-                                                                               dones);
-    attn_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(G, O, D, row_denom, pair_denom, out,
+                                                                               dones, partials);
+    attn_fin_kernel<<<1, 64, 0, static_cast<hipStream_t>(stream)>>>(partials, G, O, D, row_denom, pair_denom, out,
                                                                     used_denoms);
     return status();
 }
@@ -582,13 +603,14 @@ int32_t swarm_oc2_attention_terms_backward(int32_t B, int32_t L, int32_t O, int3
 int32_t swarm_oc2_action_terms(int64_t M, int32_t A, int32_t squashed, const float* means, const float* stds,
                                const float* ref_means, const float* ref_stds, const float* actions,
                                const float* old_log_probs, const uint8_t* loss_mask, const float* row_denom,
-                               float* log_probs, float* ref_log_probs, float* out, float* used_denom, void* stream) {
+                               float* log_probs, float* ref_log_probs, float* out, float* used_denom,
+                               int32_t* bad_inputs, void* stream) {
     if (M < 1 || A < 1 || !means || !stds || !ref_means || !ref_stds || !actions || !old_log_probs || !loss_mask ||
         !log_probs || !ref_log_probs || !out || !used_denom)
         return SWARM_ERR_ARG;
     action_fwd_kernel<<<1, kThreads, 0, static_cast<hipStream_t>(stream)>>>(
         M, A, squashed, means, stds, ref_means, ref_stds, actions, old_log_probs, loss_mask, row_denom, log_probs,
-        ref_log_probs, out, used_denom);
+        ref_log_probs, out, used_denom, bad_inputs);
     return status();
 }
 

@@ -33,12 +33,17 @@ __global__ __launch_bounds__(kThreads) void list_copy_kernel(const uint64_t* __r
 
 // Stream gate: one lane polls a host-coherent word until the host sets it (or the wall clock,
 // 100 MHz, passes the limit: every launch of it ends), so the work enqueued behind it runs
-// back to back from the release on, without the host's launch latency in between.
-__global__ __launch_bounds__(64) void gate_kernel(const uint32_t* flag, uint64_t limit_ticks) {
+// back to back from the release on, without the host's launch latency in between. A release
+// on the time limit is reported in word 1 (a vector store to the host-coherent buffer), so the
+// host can tell that the gated work started before it released the flag.
+__global__ __launch_bounds__(64) void gate_kernel(uint32_t* flag, uint64_t limit_ticks) {
     if (threadIdx.x != 0) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == 0u) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > limit_ticks) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit_ticks) {
+            __hip_atomic_store(flag + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
         __builtin_amdgcn_s_sleep(8);
     }
 }
@@ -50,7 +55,8 @@ extern "C" int32_t swarm_gate_alloc(uint32_t** flag) {
     *flag = nullptr;
     void* p = nullptr;
     if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return SWARM_ERR_HIP;
-    *static_cast<volatile uint32_t*>(p) = 0u;
+    static_cast<volatile uint32_t*>(p)[0] = 0u;   // the release flag
+    static_cast<volatile uint32_t*>(p)[1] = 0u;   // set by the gate when it released on its time limit
     *flag = static_cast<uint32_t*>(p);
     return SWARM_OK;
 }
@@ -62,7 +68,8 @@ extern "C" int32_t swarm_gate_free(uint32_t* flag) {
 
 extern "C" int32_t swarm_gate_wait(const uint32_t* flag, int64_t timeout_us, void* stream) {
     if (!flag || timeout_us < 0 || timeout_us > 60000000) return SWARM_ERR_ARG;
-    hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, (uint64_t)timeout_us * 100u);
+    hipLaunchKernelGGL(gate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, const_cast<uint32_t*>(flag),
+                       (uint64_t)timeout_us * 100u);
     return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP;
 }
 

@@ -75,11 +75,18 @@ def test_capacity_and_overflow():
     buf = POCARolloutBuffer(T, E, N, obs_dim=2, act_dim=1, memory_size=2, device="cpu", chunk_length=16,
                             episode_decisions=30)
     S = buf.start_slots
+    failed_at = None
     for t in range(T):
-        buf.put_start("memory_h", t, torch.ones(E, N, 2) * t)
         buf.dones[t] = 1.0                               # an episode end every row
+        try:
+            buf.put_start("memory_h", t, torch.ones(E, N, 2) * t)
+        except RuntimeError as e:                        # fail fast: within OVERFLOW_CHECK_ROWS rows
+            assert "chunk-start slots" in str(e)
+            failed_at = t
+            break
+    assert failed_at is not None and failed_at < buf.OVERFLOW_CHECK_ROWS
     assert buf._overflow.all()
-    assert int(buf._n_slots.max()) == T and buf.memory_h.shape[0] == S + 1
+    assert int(buf._n_slots.max()) == failed_at + 1 and buf.memory_h.shape[0] == S + 1
     buf.reset()
     assert not buf._overflow.any() and int(buf._n_slots.max()) == 0 and (buf.slot_of_row < 0).all()
 

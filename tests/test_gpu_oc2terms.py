@@ -169,3 +169,71 @@ def test_action_terms(squash, with_denom, gpu_device):
                      mu.grad.clone(), sd.grad.clone()))
     for k, what in enumerate(("log_prob", "ref log_prob", "kl / behaviour / entropy", "d means", "d stds")):
         _close(outs[0][k], outs[1][k], 3e-6, what)
+
+
+def test_input_checks_flag_what_torch_distributions_reject(gpu_device):
+    """An option outside [0, O) (Categorical.log_prob raises) and a non-positive / non-finite std
+    (Normal's validation raises) are flagged by the fused kernels and raised by the once-per-update
+    check; clean inputs leave the flag clear."""
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+    from SwarmACB_isaac.agents._trainer import check_policy_inputs
+    from SwarmACB_isaac.agents.learned_option_critic_networks import LearnedOptionActor
+
+    check_policy_inputs(gpu_device)
+    g = torch.Generator(device=gpu_device).manual_seed(5)
+    B, L, O, A = 4, 16, 6, 2
+    q = torch.randn(B, L, O, device=gpu_device, generator=g)
+    options = torch.randint(0, O, (B, L), device=gpu_device, generator=g)
+    mask = torch.ones(B, L, dtype=torch.bool, device=gpu_device)
+
+    class Actor:
+        epsilon_greedy_selector = True
+
+    LT.fused_option_terms(Actor(), q, options, mask, mask, 0.1, None)
+    check_policy_inputs(gpu_device)                                   # clean
+    bad = options.clone()
+    bad[1, 3] = -1                                                    # the 'fresh option' sentinel
+    LT.fused_option_terms(Actor(), q, bad, mask, mask, 0.1, None)
+    with pytest.raises(IndexError):
+        check_policy_inputs(gpu_device)
+    check_policy_inputs(gpu_device)                                   # the check reset the flag
+
+    actor = LearnedOptionActor(24, A, O, hidden=16, option_hidden=16, option_memory_size=8, memory_size=16,
+                               squash_actions=True).to(gpu_device)
+    means = torch.randn(B, L, O, A, device=gpu_device, generator=g) * 0.5
+    stds = torch.rand(B, L, O, A, device=gpu_device, generator=g) * 0.5 + 0.1
+    actions = torch.tanh(torch.randn(B, L, A, device=gpu_device, generator=g))
+    old_lp = torch.randn(B, L, A, device=gpu_device, generator=g)
+    LT.fused_action_terms(actor, means, stds, means, stds, options, actions, old_lp, mask, None)
+    check_policy_inputs(gpu_device)
+    for v in (0.0, float("nan")):
+        s2 = stds.clone()
+        s2[2, 5, options[2, 5]] = v                                      # the selected option's std
+        LT.fused_action_terms(actor, means, s2, means, stds, options, actions, old_lp, mask, None)
+        with pytest.raises(ValueError):
+            check_policy_inputs(gpu_device)
+
+
+def test_attention_terms_concurrent_streams(gpu_device):
+    """Two attention / option forwards in flight on two streams at once each reduce through their
+    own workspace (the partials were a single library buffer before): both equal their
+    one-at-a-time results bit for bit."""
+    from SwarmACB_isaac.agents import learned_option_critic_trainer as LT
+
+    g = torch.Generator(device=gpu_device).manual_seed(9)
+    B, L, O, D = 32, 128, 6, 24
+    xs = [torch.sigmoid(torch.randn(B, L, O, D, device=gpu_device, generator=g)) for _ in range(2)]
+    mask = torch.rand(B, L, device=gpu_device, generator=g) > 0.2
+    dones = (torch.rand(B, L, device=gpu_device, generator=g) > 0.9).float()
+    alone = [torch.stack(LT.fused_attention_terms(x, mask, dones, None, None)) for x in xs]
+    torch.cuda.synchronize(gpu_device)
+    streams = [torch.cuda.Stream(gpu_device) for _ in xs]
+    outs = [None, None]
+    for _ in range(20):
+        for k, (x, s) in enumerate(zip(xs, streams)):
+            s.wait_stream(torch.cuda.current_stream(gpu_device))
+            with torch.cuda.stream(s):
+                outs[k] = torch.stack(LT.fused_attention_terms(x, mask, dones, None, None))
+        torch.cuda.synchronize(gpu_device)
+        for k in range(2):
+            assert torch.equal(outs[k], alone[k])

@@ -19,6 +19,16 @@ import sys
 from collections import defaultdict
 
 
+def _sha256(path: str) -> str | None:
+    import hashlib
+
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def read_pass(d: str) -> tuple[dict, dict]:
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     per = defaultdict(lambda: defaultdict(float))
@@ -42,7 +52,7 @@ def read_pass(d: str) -> tuple[dict, dict]:
 
 def main(root: str):
     out = {"passes": {}}
-    for name in ("fetch", "write", "sq1", "sq2"):
+    for name in ("fetch", "write", "sq1", "sq2", "sq3"):
         avg, meta = read_pass(os.path.join(root, name))
         out["passes"][name] = avg
         if meta:
@@ -70,6 +80,28 @@ def main(root: str):
                 res[k.lower() + "_frac"] = c[k] / wc
     if "SQ_INSTS_VALU" in c:
         res["valu_insts_per_launch"] = c["SQ_INSTS_VALU"]
+    # VALUBusy / VALUUtilization as rocprofv3's derived expressions (gfx94x formulas, which ROCm 7.2
+    # also applies to gfx950): 100 * sum(SQ_ACTIVE_INST_VALU) / CU_NUM / max(GRBM_GUI_ACTIVE) and
+    # sum(SQ_THREAD_CYCLES_VALU) / (sum(SQ_ACTIVE_INST_VALU) * 64). GRBM_GUI_ACTIVE is summed over
+    # the 8 XCDs here (MI355X_MICROARCH.md, DVFS give-back), so the per-XCD clock count is / 8.
+    s3 = out["passes"].get("sq3") or {}
+    if s3.get("GRBM_GUI_ACTIVE") and s3.get("SQ_ACTIVE_INST_VALU"):
+        cyc = s3["GRBM_GUI_ACTIVE"] / 8.0
+        res["valu_busy"] = s3["SQ_ACTIVE_INST_VALU"] / 256.0 / cyc
+        res["gpu_cycles_per_launch"] = cyc
+        if s3.get("SQ_THREAD_CYCLES_VALU"):
+            res["valu_utilization"] = s3["SQ_THREAD_CYCLES_VALU"] / (s3["SQ_ACTIVE_INST_VALU"] * 64.0)
+        if "SQ_ACTIVE_INST_VALU2" in s3:
+            res["valu_dual_issue_frac"] = s3["SQ_ACTIVE_INST_VALU2"] / s3["SQ_ACTIVE_INST_VALU"]
+        if s3.get("SQ_INSTS_VALU"):
+            res["valu_trans_frac"] = s3.get("SQ_INSTS_VALU_TRANS_F32", 0.0) / s3["SQ_INSTS_VALU"]
+            # issue floor of the launch: every SIMD's waves at 2 cycles per wave64 VALU instruction
+            # (MI355X_MICROARCH.md, v_fma_f32 throughput) over the 1,024 SIMDs, vs the clocks it took
+            res["valu_issue_floor_frac"] = s3["SQ_INSTS_VALU"] * 2.0 / 1024.0 / cyc
+        if s3.get("SQ_BUSY_CU_CYCLES"):
+            res["cu_busy_frac"] = s3["SQ_BUSY_CU_CYCLES"] * 4.0 / 256.0 / cyc
+        if s3.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in s3:
+            res["sq3_wait_any_frac"] = s3["SQ_WAIT_ANY"] / s3["SQ_WAVE_CYCLES"]
     out["derived"] = res
     out["counters"] = c
     print(json.dumps(out, indent=1, sort_keys=True))
@@ -87,6 +119,9 @@ if __name__ == "__main__":
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--substeps", type=int, default=5)
     ap.add_argument("--layout", type=int, default=0)
+    ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                "swarmacb-isaaclab_amd", "SwarmACB_isaac", "libswarmstep.so"),
+                    help="the library the passes ran (its sha256 stamps the record)")
     a = ap.parse_args()
     o = main(a.root)
     if a.traffic_json:
@@ -95,6 +130,10 @@ if __name__ == "__main__":
                "hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
                "fetch_bytes_raw": d.get("fetch_bytes_raw"), "write_bytes": d.get("write_bytes"),
                "valu_insts_per_launch": d.get("valu_insts_per_launch"),
+               "valu_busy": d.get("valu_busy"), "valu_utilization": d.get("valu_utilization"),
+               "valu_issue_floor_frac": d.get("valu_issue_floor_frac"),
+               "sq_wait_any_frac": d.get("sq_wait_any_frac"),
+               "lib_sha256": _sha256(a.lib),
                "kernel_resources": o.get("kernel_resources"),
                "method": "rocprofv3 --pmc, one counter group per pass (FETCH_SIZE, WRITE_SIZE, SQ_*), "
                          "averaged over step_kernel dispatches; FETCH_SIZE x2 (gfx950 half-count), KiB -> B"}
