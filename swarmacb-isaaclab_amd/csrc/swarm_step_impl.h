@@ -38,53 +38,27 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
-// 1: wave-uniform pre-filters skip wall faces / inside tests no lane can need
-// (results unchanged); 0: every face evaluated (reference loop shape).
-#ifndef SWARM_WALL_FILTER
-#define SWARM_WALL_FILTER 1
-#endif
-
-// 1: a part's compile-time neighbour chunk is read from LDS back to back and
-// its candidate bits are formed branch-free (one LDS wait, no exec-mask
-// bookkeeping per neighbour); 0: per-neighbour loop with a divergent exit.
-#ifndef SWARM_BRANCHFREE_CHUNKS
-#define SWARM_BRANCHFREE_CHUNKS 1
-#endif
-
-// 1: the contact solver skips the partial-sum exchange when no lane of a wave
-// met a candidate pair, and stops iterating at a fixed point (results unchanged)
-#ifndef SWARM_SOLVE_SHORTCUTS
-#define SWARM_SOLVE_SHORTCUTS 1
-#endif
-
-// 1: single-wave workgroups exchange through LDS without hardware waits (sync_wg)
-#ifndef SWARM_WAVE_SYNC
-#define SWARM_WAVE_SYNC 1
-#endif
-
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
 #endif
 
-// Wave priority for arenas with live contacts. A launch lasts as long as its
-// slowest wave, and the slowest waves are the arenas whose contact solver keeps
-// moving robots (up to 25 push iterations per launch against 9 on average,
-// tools/wave_timing.py). 2: graded s_setprio 1 / 2 / 3 after T / 2T / 3T solver
-// iterations that moved a robot, so those waves win the SIMD's issue
-// arbitration over co-resident waves with slack; 0: off. Scheduling only: the
-// results are bitwise the same.
-#ifndef SWARM_PRIO_MODE
-#define SWARM_PRIO_MODE 2
-#endif
-#ifndef SWARM_PRIO_T
-#define SWARM_PRIO_T 2
-#endif
-// 1: sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual
-// correction (bitwise = sqrtf); 0: the library's sqrtf.
-#ifndef SWARM_CR_SQRT
-#define SWARM_CR_SQRT 1
-#endif
+// Work the wave skips without changing a result (rounds 2-4; the measured
+// alternatives live in git history and profiles/):
+//  * wave-uniform pre-filters skip arena-wall faces and "strictly inside" tests no lane can need;
+//  * a part's compile-time neighbour chunk is read from LDS back to back and its candidate bits
+//    are formed branch-free (one LDS wait, no exec-mask bookkeeping per neighbour);
+//  * the contact solver skips the partial-sum exchange when no lane of a wave met a candidate
+//    pair, and stops iterating at a fixed point;
+//  * single-wave workgroups exchange through LDS without hardware waits (sync_wg);
+//  * wave priority for arenas with live contacts: a launch lasts as long as its slowest wave, and
+//    the slowest waves are the arenas whose contact solver keeps moving robots (up to 25 push
+//    iterations per launch against 9 on average, tools/wave_timing.py), so a wave raises its
+//    s_setprio to 1 / 2 / 3 after kPrioT / 2 kPrioT / 3 kPrioT solver iterations that moved a
+//    robot and wins the SIMD's issue arbitration over co-resident waves with slack (scheduling
+//    only: the results are bitwise the same);
+//  * sqrt of known-normal positive arguments as hardware sqrt + one-ulp residual correction
+//    (bitwise = sqrtf).
 
 // Arithmetic shortcuts of the product kernel, all inside the parity contract (DESIGN.md §4,
 // round 4; the measured alternatives are recorded in profiles/r04/step/):
@@ -109,35 +83,6 @@ namespace swarm {
 
 // kGeomTab[mission][profile]: compile-time copy of build_geom() (gen_tables.cpp)
 #include "swarm_geom_tables.inc"
-
-#if SWARM_WAVE_TIMING
-// per wave: {start clock lo, end - start, HW_ID, XCC_ID}, {wall start lo, wall end lo, solver passes, work},
-// {work counters}, then kWtPhases shader-clock sums of the phases below (4 uint4)
-constexpr int kWaveLogMax = 65536;
-constexpr int kWaveLogRow = 7;
-enum WtPhase : int {
-    PH_ACT_INT = 0,   // actions + integrate (+ the decimation sincos)
-    PH_SOLVE,         // env.step contact solver (all passes; includes the PH_PUSH_* below)
-    PH_RESOLVE,       // the all-env re-solve after a time-out (DG:1262)
-    PH_REWARD,        // dones, rewards, terminal critic, spawn
-    PH_PUBLISH,       // observation: position tile + inside flags + exchange point
-    PH_PROX,          // proximity partial (walls + robot discs)
-    PH_RAB,           // range-and-bearing partial (LOS, packet loss draws)
-    PH_COMBINE,       // partial-sum exchange of the 3 lanes of a robot
-    PH_FINISH,        // aggregates, light, ground, observation stores
-    PH_PUSH_PUB,      // push: position publish + exchange point
-    PH_PUSH_CAND,     // push: candidate mask of the lane's neighbour chunk
-    PH_PUSH_PAIRS,    // push: exact pair terms of the candidates
-    PH_PUSH_XCHG,     // push: partial-sum exchange and update
-    kWtPhases
-};
-static __device__ uint4 g_wave_log[kWaveLogRow * kWaveLogMax];
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m));
-    return v;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 //  Philox4x32-10 (counter-based: results depend only on (seed, counter), so
@@ -212,15 +157,11 @@ __device__ __forceinline__ float fsqrt(float v) { return __builtin_amdgcn_sqrtf(
 // moved by one ulp where the residual says so, without the library
 // expansion's denormal scaling and inf / zero class fix-ups.
 __device__ __forceinline__ float nsqrt(float v) {
-#if SWARM_CR_SQRT
     const float r = __builtin_amdgcn_sqrtf(v);
     const float dn = __uint_as_float(__float_as_uint(r) - 1u), up = __uint_as_float(__float_as_uint(r) + 1u);
     float o = fmaf(-dn, r, v) <= 0.0f ? dn : r;
     o = fmaf(-up, r, v) > 0.0f ? up : o;
     return o;
-#else
-    return sqrtf(v);
-#endif
 }
 
 __device__ __forceinline__ float sgnf(float v) { return v > 0.0f ? 1.0f : (v < 0.0f ? -1.0f : 0.0f); }
@@ -272,27 +213,10 @@ struct Lane {
     unsigned long long amask;  // ballot bits of this arena's part-0 lanes
     int E, obs_dim;            // runtime layout (kernel argument)
     uint32_t seed_lo, seed_hi;
-#if SWARM_PRIO_MODE
     mutable int moved_iters;   // wave-uniform count of solver iterations that moved a robot
     mutable int prio;          // wave-uniform current s_setprio level
-#endif
-#if SWARM_WAVE_TIMING
-    mutable uint32_t wt_push, wt_pair, wt_rab, wt_seg, wt_disc;   // per-lane work counters (diagnostic)
-    mutable uint32_t wt_ph[kWtPhases];                            // shader clocks per phase (diagnostic)
-#endif
+    SWARM_WT_LANE_FIELDS       // diagnostic build only (swarm_diag.h)
 };
-#if SWARM_WAVE_TIMING
-#define SWARM_WT(stmt) stmt
-// phase stamps: SWARM_PH_T(t) opens, SWARM_PH_ADD(L, k, t) charges the clocks since t to phase k
-#define SWARM_PH_T(t) uint64_t t = __builtin_amdgcn_s_memtime()
-#define SWARM_PH_ADD(L, k, t) ((L).wt_ph[k] += (uint32_t)(__builtin_amdgcn_s_memtime() - (t)))
-#define SWARM_PH_NEXT(L, k, t) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); (L).wt_ph[k] += (uint32_t)(_n - (t)); t = _n; } while (0)
-#else
-#define SWARM_WT(stmt)
-#define SWARM_PH_T(t)
-#define SWARM_PH_ADD(L, k, t)
-#define SWARM_PH_NEXT(L, k, t)
-#endif
 
 // Philox counter (global env, robot | block << 8 | purpose << 24, tick), key = seed.
 __device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t block, uint32_t purpose,
@@ -323,7 +247,7 @@ struct Shared {
 // s_waitcnt / s_barrier). Multi-wave layouts need the real barrier.
 template <int LY>
 __device__ __forceinline__ void sync_wg() {
-    if constexpr (ly_waves(LY) == 1 && SWARM_WAVE_SYNC) {
+    if constexpr (ly_waves(LY) == 1) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     } else {
@@ -346,15 +270,14 @@ __device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
     sync_wg<LY>();   // the solver reads the wall tables before any other exchange point
 }
 
-#if SWARM_PRIO_MODE == 2
-// one more unit of wave-uniform work seen: raise the priority at T, 2T, 3T units
+// one more unit of wave-uniform work seen: raise the priority at kPrioT, 2 kPrioT, 3 kPrioT units
+constexpr int kPrioT = 2;
 __device__ __forceinline__ void prio_bump(const Lane& L) {
     const int c = ++L.moved_iters;
-    if (c == SWARM_PRIO_T && L.prio < 1) { __builtin_amdgcn_s_setprio(1); L.prio = 1; }
-    if (c == 2 * SWARM_PRIO_T && L.prio < 2) { __builtin_amdgcn_s_setprio(2); L.prio = 2; }
-    if (c == 3 * SWARM_PRIO_T && L.prio < 3) { __builtin_amdgcn_s_setprio(3); L.prio = 3; }
+    if (c == kPrioT && L.prio < 1) { __builtin_amdgcn_s_setprio(1); L.prio = 1; }
+    if (c == 2 * kPrioT && L.prio < 2) { __builtin_amdgcn_s_setprio(2); L.prio = 2; }
+    if (c == 3 * kPrioT && L.prio < 3) { __builtin_amdgcn_s_setprio(3); L.prio = 3; }
 }
-#endif
 
 __device__ __forceinline__ int arena_count(const Lane& L, bool pred) {
     const unsigned long long m = __ballot(pred);
@@ -514,7 +437,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         cx += row ? 0.0f : -hx;
         cy += row ? 0.0f : -hy;
     };
-    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+    if constexpr (C > 0) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
         const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float px, float py) {
             float dx, dy;
@@ -544,7 +467,7 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
         }
     }
     if constexpr (ly_parts(LY) > 1) {
-        if constexpr (ly_waves(LY) == 1 && SWARM_SOLVE_SHORTCUTS) {
+        if constexpr (ly_waves(LY) == 1) {
             // no lane of the wave met a candidate: every partial is +0, and
             // (x + 0) - 0 is what the exchange below would produce
             if (!__any(rx != 0.0f || ry != 0.0f || cx != 0.0f || cy != 0.0f)) {
@@ -728,7 +651,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
             }
         }
         gate_walls<MISSION, ISAAC>(g, x, y);
-        if constexpr (ly_waves(LY) == 1 && SWARM_SOLVE_SHORTCUTS) {
+        if constexpr (ly_waves(LY) == 1) {
             // Fixed point: if no robot of the wave's arenas moved in a middle
             // iteration, every later middle iteration (same body) maps the same
             // positions to themselves. The last iteration (no push) is a no-op
@@ -746,9 +669,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
                 }
                 fixed = true;
             }
-#if SWARM_PRIO_MODE == 2
             if (middle && moved) prio_bump(L);
-#endif
         }
     }
 #undef SOLVE_WALLS
@@ -803,7 +724,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     // for them, so the wave loops max(near) times (usually 0-1), not once per
     // segment of the part. Max is order-free: the readings are unchanged.
     uint32_t near_mask = 0;
-#if SWARM_BRANCHFREE_CHUNKS
     // every lane tests all faces (compile-time constants, a fused estimate of sd
     // with a 1e-4 margin: the filter only widens) and keeps its part's share
     constexpr uint32_t part0 = [] {
@@ -836,22 +756,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         near_mask |= dx * dx + dy * dy < (g.prox_range + 1e-3f) * (g.prox_range + 1e-3f) ? (1u << (12 + k)) : 0u;
     }
     near_mask &= part0 << L.p;
-#else
-    for (int s = L.p; s < g.nseg; s += ly_parts(LY)) {
-        bool near;
-        if (s < 12) {
-            const float sd = (x - g.face_px[s]) * g.face_nx[s] + (y - g.face_py[s]) * g.face_ny[s];
-            near = sd < g.prox_range + 1e-3f;
-        } else {
-            const int k = s - 12;
-            const float rx = x - g.iw_ax[k], ry = y - g.iw_ay[k];
-            const float u = clampf((rx * g.iw_tx[k] + ry * g.iw_ty[k]) / g.iw_lsq[k], 0.0f, 1.0f);
-            const float dx = x - (g.iw_ax[k] + u * g.iw_tx[k]), dy = y - (g.iw_ay[k] + u * g.iw_ty[k]);
-            near = dx * dx + dy * dy < (g.prox_range + 1e-3f) * (g.prox_range + 1e-3f);
-        }
-        if (near) near_mask |= 1u << s;
-    }
-#endif
     while (near_mask) {
         SWARM_WT(L.wt_seg++);
         const int s = __builtin_ctz(near_mask);
@@ -882,7 +786,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const bool pre = (proj > 0.0f) & (csq <= g.r2);
             // a disc spans at most two of the 45-degree rays: the wave skips the rest
             // (a ray no active lane can hit leaves every reading unchanged)
-            if (SWARM_WALL_FILTER && !__any(pre)) continue;
+            if (!__any(pre)) continue;
             const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
             const float hd = fmaxf(proj - hc, 0.0f);
             const bool hit = pre & (hd <= g.prox_range);
@@ -890,7 +794,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
     };
-    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS) {
+    if constexpr (C > 0) {
         const uint32_t cand = disc_cand ? *disc_cand
                                         : chunk_mask<C>(L, S.xy, x, y,
                                                         [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
@@ -1027,7 +931,7 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         axx += aw * cb;
         ayy += aw * sb;
     };
-    if constexpr (C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18) {
+    if constexpr (C > 0 && ChunkRng<C>::K18) {
         // as the K18 path below: every candidate's packet-loss uniform first (one
         // Philox block per chunk), then the term for the kept neighbours in increasing j
         const uint32_t cand = pre_cand ? *pre_cand : chunk_mask<C>(L, xy, x, y, [&](float dx, float dy) {
@@ -1248,7 +1152,6 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 template <int LY>
 __device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y) {
     bool ins = true;
-#if SWARM_WALL_FILTER
     // |p| < apothem - 1e-3 - margin implies every face is > 1e-3 away; the flag
     // only selects a shortcut (a robot flagged "not inside" gets the full,
     // exact line-of-sight test), so the conservative radius keeps results exact
@@ -1257,11 +1160,6 @@ __device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>
         for (int k = 0; k < 12; ++k)
             ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
     }
-#else
-#pragma unroll
-    for (int k = 0; k < 12; ++k)
-        ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
-#endif
     if (L.p == 0) {
         S.xy[L.r] = make_float2(x, y);
         S.ins[L.r] = ins ? 1 : 0;
@@ -1341,7 +1239,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     }
     float prox[8], lt[8], r4[4], zt;
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
-    constexpr bool FUSE = C > 0 && SWARM_BRANCHFREE_CHUNKS && ChunkRng<C>::K18 && SWARM_ABLATE == 0;
+    constexpr bool FUSE = C > 0 && ChunkRng<C>::K18 && SWARM_ABLATE == 0;
     uint32_t mprox = 0, mrab = 0;
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
@@ -1557,15 +1455,9 @@ __device__ __forceinline__ Lane make_lane(const Geom& g, int blk) {   // g: the 
         for (int q = 0; q < L.N; ++q) m |= 1ull << (L.a * KL * L.N + q * KL);
     }
     L.amask = m;
-#if SWARM_PRIO_MODE
     L.moved_iters = 0;
     L.prio = 0;
-#endif
-#if SWARM_WAVE_TIMING
-    L.wt_push = L.wt_pair = L.wt_rab = L.wt_seg = L.wt_disc = 0;
-#pragma unroll
-    for (int k = 0; k < kWtPhases; ++k) L.wt_ph[k] = 0;
-#endif
+    SWARM_WT_LANE_INIT(L);
     return L;
 }
 
@@ -1576,10 +1468,7 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
     const Geom gr, const DevState st, const void* __restrict__ actions, const float* __restrict__ ovr,
     const DevOut out, const DevReplay rp_in, uint64_t tick0, int n_sub, uint64_t reset_any) {
     const DevReplay rp = REPLAY ? rp_in : DevReplay{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
-#if SWARM_WAVE_TIMING
-    const uint64_t wt_c0 = __builtin_amdgcn_s_memtime();
-    const uint64_t wt_w0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    SWARM_WT_KERNEL_BEGIN();
     const Geom& g = kGeomTab[MISSION][PROFILE];   // mission constants as literals; gr: runtime fields
     constexpr int C = NA > 0 ? (NA + ly_parts(LY) - 1) / ly_parts(LY) : 0;   // neighbour chunk per part (0 = runtime)
     __shared__ Shared<LY> S;
@@ -1765,35 +1654,8 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
             if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
         }
     }
-#if SWARM_WAVE_TIMING
-    if constexpr (!REPLAY && ly_waves(LY) == 1) {
-        const uint64_t wt_c1 = __builtin_amdgcn_s_memtime();
-        const uint64_t wt_w1 = __builtin_amdgcn_s_memrealtime();
-        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
-        const uint32_t push = wave_max(L.wt_push), pair = wave_max(L.wt_pair), rab = wave_max(L.wt_rab);
-        const uint32_t seg = wave_max(L.wt_seg), disc = wave_max(L.wt_disc);
-        if (threadIdx.x == 0 && blockIdx.x < kWaveLogMax) {
-            uint4* row = g_wave_log + kWaveLogRow * blockIdx.x;
-            row[0] = make_uint4((uint32_t)wt_c0, (uint32_t)(wt_c1 - wt_c0), hw, xcc);
-            row[1] = make_uint4((uint32_t)wt_w0, (uint32_t)wt_w1, push, pair);
-            row[2] = make_uint4(rab, seg, disc, 0u);
-            uint32_t ph[16] = {};
-#pragma unroll
-            for (int k = 0; k < kWtPhases; ++k) ph[k] = L.wt_ph[k];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) row[3 + k] = make_uint4(ph[4 * k], ph[4 * k + 1], ph[4 * k + 2], ph[4 * k + 3]);
-        }
-    }
-#endif
+    if constexpr (!REPLAY && ly_waves(LY) == 1) SWARM_WT_KERNEL_END(L);
 }
-
-#if SWARM_WAVE_TIMING
-static int read_wave_log(void* host, size_t bytes) {
-    const size_t n = bytes < sizeof(g_wave_log) ? bytes : sizeof(g_wave_log);
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_log), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 //  Reset kernel: _reset_idx(mask) + observations (DirectMARLEnv.reset)

@@ -21,9 +21,13 @@ tensorboard's SummaryWriter, absent here, is a no-op). Recorded as data:
   before ``optimizer.step()`` and every parameter after it;
 * the metrics ``update()`` returned.
 
-Cases: ``oc_update`` (small networks, collect + update) and ``oc_collect_h128``
+Cases: ``oc_update`` (small networks, collect + update), ``oc_collect_h128``
 (critic hidden 128 / 4 heads, the size the fused critic kernel serves; collect
-only).
+only), ``oc_update_h128`` (configs/OC_DirGate_cyclamen.yaml network sizes, 20
+e-pucks, sequence length 2) and ``oc_update_h128_L128`` (the same networks at the
+config's sequence_length 128, OC_DirGate_cyclamen.yaml:38, with an episode that
+ends mid-chunk; only the chunk-start rows of the start-read memories are kept in
+the file, option_critic_buffer.py:169-277).
 
 Usage: python tests/golden/trainer/make_oc_golden.py
 """
@@ -104,8 +108,31 @@ STATE_KEYS = ("manager_memory_h", "manager_memory_c", "value_memory_h", "value_m
               "joint_memory_c", "baseline_memory_h", "baseline_memory_c", "current_options")
 
 
-def run_case(OCT, name, *, E, N, D, R, dp, cfg_kw, seed, do_update):
+START_ROW_KEYS = ("memory_h", "memory_c", "value_memory_h", "value_memory_c", "joint_memory_h", "joint_memory_c",
+                  "baseline_memory_h", "baseline_memory_c")
+
+
+def chunk_start_rows(dones, L):
+    """(T, E) mask of the rows get_sequence_batches reads the START_ROW_KEYS memories from: the
+    chunk starts of every episode segment (option_critic_buffer.py:169-213)."""
+    T, E = dones.shape
+    L = max(1, min(int(L), T))
+    m = np.zeros((T, E), bool)
+    for e in range(E):
+        start = 0
+        ends = [t + 1 for t in range(T) if dones[t, e] > 0.5]
+        if not ends or ends[-1] != T:
+            ends.append(T)
+        for end in ends:
+            m[start:end:L, e] = True
+            start = end
+    return m
+
+
+def run_case(OCT, name, *, E, N, D, R, dp, cfg_kw, seed, do_update, extra_truncations=(), start_rows_only=False):
     env = CyclamenScriptedEnv(E, N, D, dp * R, seed)
+    for k, e in extra_truncations:          # (substep, env) time-outs added to the script
+        env.trunc[k, e] = True
     cfg = OCT.FixedOptionCriticConfig(horizon=R, decision_period=dp, log_dir="/tmp/_oc_runs",
                                       checkpoint_dir="/tmp/_oc_ckpt", **cfg_kw)
     torch.manual_seed(seed)
@@ -133,6 +160,13 @@ def run_case(OCT, name, *, E, N, D, R, dp, cfg_kw, seed, do_update):
     out["ptr"] = np.int64(T)
     for k in BUF_KEYS:
         out[f"buf/{k}"] = getattr(b, k)[:T].numpy().copy()
+    if start_rows_only:
+        # the sequence batcher reads these memories only at chunk starts: the other rows are zeroed
+        # in the file (they compress away; a trainer that read them would fail the test)
+        keep = chunk_start_rows(out["buf/dones"], cfg_kw["sequence_length"])
+        for k in START_ROW_KEYS:
+            out[f"buf/{k}"][~keep] = 0.0
+        out["start_rows_only"] = np.int64(1)
     for k in STATE_KEYS:
         out[f"state/{k}"] = getattr(tr, k).numpy().copy()
     out["global_step"] = np.int64(tr.global_step)
@@ -211,6 +245,18 @@ def main(only=()):
             cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2,
                         critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=160,
                         num_epochs=1)),
+        # the same networks at the config's real sequence length (OC_DirGate_cyclamen.yaml:38): 3 envs x
+        # 140 decisions; besides the script's early time-outs (env 1 in decision 0, env 2 in decisions 1-2)
+        # env 0 times out at decision 70 and all at the last one -> chunks [0,71) [71,140) | [0,1) [1,129)
+        # [129,140) | ...: full-length, partial and one-step sequences, zero padding, memories taken at
+        # chunk starts after an episode end; 50 sequences per minibatch (1 epoch, the partial last
+        # minibatch dropped as the reference does); schedules far from their end so Adam moves the weights
+        "oc_update_h128_L128": lambda: run_case(
+            OCT, "oc_update_h128_L128", E=3, N=20, D=4, R=140, dp=5, seed=14, do_update=True,
+            cfg_kw=dict(common, hidden_dim=128, num_layers=1, memory_size=128, sequence_length=128,
+                        critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=6400,
+                        num_epochs=1, total_timesteps=10_000_000),
+            extra_truncations=((5 * 70 + 2, 0),), start_rows_only=True),
     }
     for name, fn in cases.items():
         if not only or name in only:

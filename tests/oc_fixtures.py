@@ -35,8 +35,13 @@ OC_CASES = {
     # configs/OC_DirGate_cyclamen.yaml network sizes, 20 e-pucks
     "oc_update_h128": dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=2, critic_hidden_dim=128,
                            critic_num_layers=1, critic_num_heads=4, mini_batch_size=160, num_epochs=1),
+    # the same networks at the config's sequence_length 128 (OC_DirGate_cyclamen.yaml:38), an episode ending
+    # mid-chunk; only the chunk-start rows of the start-read memories are in the file
+    "oc_update_h128_L128": dict(hidden_dim=128, num_layers=1, memory_size=128, sequence_length=128,
+                                critic_hidden_dim=128, critic_num_layers=1, critic_num_heads=4, mini_batch_size=6400,
+                                num_epochs=1, total_timesteps=10_000_000),
 }
-UPDATE_CASES = ("oc_update", "oc_update_h128")
+UPDATE_CASES = ("oc_update", "oc_update_h128", "oc_update_h128_L128")
 OC_LOSS_NAMES = ("policy", "value", "joint_option_value", "baseline", "termination", "option_entropy",
                  "termination_entropy", "mean_beta", "mean_option_advantage")
 

@@ -61,7 +61,8 @@ for k in ('default', 'driver_args'):
     bash tools/variants.sh run > $OUT/variants.log 2>&1 || { tail -20 $OUT/variants.log; exit 8; }
     tail -20 $OUT/variants.log ;;
   wavetime)
-    timeout -k 10 300 python3 tools/wave_timing.py ${WT_ARGS:-} > $OUT/wave_timing.log 2>&1 || { tail -20 $OUT/wave_timing.log; exit 9; }
+    SWARMSTEP_LIB=$PWD/${WT_LIB:-build/variants/lib_wt.so} timeout -k 10 300 python3 tools/wave_timing.py ${WT_ARGS:-} \
+      > $OUT/wave_timing.log 2>&1 || { tail -20 $OUT/wave_timing.log; exit 9; }
     tail -12 $OUT/wave_timing.log ;;
   train)
     for cfg in ${CFGS:-C5 C4 C3}; do
