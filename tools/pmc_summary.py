@@ -99,7 +99,8 @@ def main(root: str):
             # (MI355X_MICROARCH.md, v_fma_f32 throughput) over the 1,024 SIMDs, vs the clocks it took
             res["valu_issue_floor_frac"] = s3["SQ_INSTS_VALU"] * 2.0 / 1024.0 / cyc
         if s3.get("SQ_BUSY_CU_CYCLES"):
-            res["cu_busy_frac"] = s3["SQ_BUSY_CU_CYCLES"] * 4.0 / 256.0 / cyc
+            # per-SE sums of per-SIMD quad-cycles: / 1,024 SIMDs x 4 cycles
+            res["simd_busy_frac"] = s3["SQ_BUSY_CU_CYCLES"] * 4.0 / 1024.0 / cyc
         if s3.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in s3:
             res["sq3_wait_any_frac"] = s3["SQ_WAIT_ANY"] / s3["SQ_WAVE_CYCLES"]
     out["derived"] = res
