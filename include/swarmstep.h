@@ -72,11 +72,15 @@ typedef struct {
     int32_t discrete_actions;     /* 1: action = behaviour-module id (int32); 0: wheels (float2) */
     int32_t max_episode_length;   /* steps; isaac ceil(episode_length_s/(dt*decimation)) */
     int32_t decimation;           /* isaac physics substeps per env.step (DGC:97) */
-    int32_t layout;               /* work layout: 0 = auto (103 when num_agents <= 21, else 4),
-                                     103 = one arena per wave, 3 lanes per robot (needs
-                                     num_agents <= 21), 4 = four waves share 64/N arenas (one lane
-                                     per robot and wave). num_envs * num_agents * 24 must stay
-                                     below 2^31. */
+    int32_t layout;               /* work layout: 0 = auto (203 for the isaac profile with continuous
+                                     actions, 20 robots and num_envs <= 8 x the device's CUs, else
+                                     103 when num_agents <= 21, else 4), 103 = one arena per wave,
+                                     3 lanes per robot (needs num_agents <= 21), 203 = two waves per
+                                     arena, a physics and an observation wave pipelined over the
+                                     substeps (isaac, continuous, 20 robots; other cases and replay
+                                     run as 103; bitwise the results of 103), 4 = four waves share
+                                     64/N arenas (one lane per robot and wave). num_envs *
+                                     num_agents * 24 must stay below 2^31. */
     int64_t env_offset;           /* global index of local env 0 (multi-GPU sharding) */
     uint64_t seed;                /* Philox key for all in-kernel randomness */
 } swarm_params_t;

@@ -135,13 +135,22 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
     if (p->num_envs < 1 || p->num_agents < 1 || p->num_agents > SWARM_MAX_AGENTS) return SWARM_ERR_ARG;
     if (p->obs_dim != 24 && p->obs_dim != 4) return SWARM_ERR_ARG;
     if (p->max_episode_length < 1 || p->decimation < 0 || p->env_offset < 0) return SWARM_ERR_ARG;
-    if (p->layout != 0 && p->layout != 4 && p->layout != 103) return SWARM_ERR_ARG;
+    if (p->layout != 0 && p->layout != 4 && p->layout != 103 && p->layout != 203) return SWARM_ERR_ARG;
     if ((int64_t)p->num_envs * p->num_agents * 24 >= ((int64_t)1 << 31)) return SWARM_ERR_ARG;  // 32-bit indices
-    if (p->layout == 103 && 3 * p->num_agents > 64) return SWARM_ERR_ARG;
+    if ((p->layout == 103 || p->layout == 203) && 3 * p->num_agents > 64) return SWARM_ERR_ARG;
     swarm_handle_t* h = new (std::nothrow) swarm_handle_t();
     if (!h) return SWARM_ERR_ARG;
     h->p = *p;
     build_geom(*p, h->g);
+    if (p->layout == 0 && p->profile == SWARM_PROFILE_ISAAC && !p->discrete_actions && p->num_agents == 20) {
+        // the two-wave pipeline (layout 203) while its 2 E waves fit at 4 per SIMD: below that
+        // occupancy an arena's dependent chain bounds layout 103's launch (swarm_step_impl.h)
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
+            (int64_t)p->num_envs <= (int64_t)cus * 4 * 2)
+            h->g.layout = 203;
+    }
     // the kernels use the compile-time tables generated from this same build_geom
     // (gen_tables.cpp); refuse to run if the library was built from stale tables
     {
@@ -273,7 +282,7 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     const hipStream_t cs = (hipStream_t)stream;
     const DevState st = dev_state(state);
     const DevOut o{out->obs, out->reward, out->truncated};
-    if (h->groups > 1 && h->g.layout == 103) {
+    if (h->groups > 1 && (h->g.layout == 103 || h->g.layout == 203)) {
         // fork: every group stream waits for the caller's stream; join: the caller's
         // stream waits for every group (one arena per workgroup, ranges of E / groups)
         if (hipEventRecord(h->gfork, cs) != hipSuccess) return hip_status();

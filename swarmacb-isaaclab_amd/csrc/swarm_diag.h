@@ -25,6 +25,33 @@
 #define SWARM_WAVE_TIMING 0
 #endif
 
+//   SWARM_ARENA_PERM=1    experiment build (tools/arena_balance.py): the step kernel's block b
+//                         runs arena g_arena_perm[b] (host-set), and records per arena the
+//                         wave-uniform count of moving solver iterations of the launch and its
+//                         block's hardware slot (HW_ID), to test cost-balanced placement.
+#ifndef SWARM_ARENA_PERM
+#define SWARM_ARENA_PERM 0
+#endif
+#if SWARM_ARENA_PERM
+namespace swarm {
+static __device__ int32_t g_arena_perm[65536];
+static __device__ int32_t g_arena_cost[65536];
+static __device__ uint32_t g_block_hw[65536];
+}  // namespace swarm
+#define SWARM_PERM_BLOCK(blk) (g_arena_perm[blk])
+#define SWARM_PERM_RECORD(L)                                                                         \
+    do {                                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < 65536) {                                                \
+            g_arena_cost[(L).env] = (L).moved_iters;                                                 \
+            g_block_hw[blockIdx.x] = __builtin_amdgcn_s_getreg((31 << 11) | 4) |                     \
+                                     (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 28);             \
+        }                                                                                            \
+    } while (0)
+#else
+#define SWARM_PERM_BLOCK(blk) (blk)
+#define SWARM_PERM_RECORD(L) ((void)0)
+#endif
+
 #if SWARM_WAVE_TIMING
 namespace swarm {
 // per wave: {start clock lo, end - start, HW_ID, XCC_ID}, {wall start lo, wall end lo, solver passes, work},

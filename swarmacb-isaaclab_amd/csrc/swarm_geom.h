@@ -71,6 +71,8 @@ enum RngPurpose : uint32_t {
     S(float, min_dist2_hi) S(float, rab_range2_hi) S(float, inv_prox_range) S(float, inv_unity)             \
     /* exact squared thresholds: fl(sqrt(s)) < R  <=>  s < x_s_lim (smallest float whose sqrt reaches R) */  \
     S(float, min_dist_s_lim) S(float, rab_s_lim)                                                            \
+    /* the same tests on s before the reference's + 1e-8: fl(s + 1e-8) < x_s_lim  <=>  s < x_pre_lim */     \
+    S(float, min_dist_pre_lim) S(float, rab_pre_lim)                                                        \
     S(float, prox_range) S(float, rab_range) S(float, rab_loss) S(float, unity) S(float, light_thr)         \
     S(float, light_int) S(float, alpha) S(float, prox_thr) S(float, pi_f) S(float, two_pi_f)                \
     S(float, half_pi_f) S(float, critic_radius)

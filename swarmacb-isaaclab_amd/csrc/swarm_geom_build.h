@@ -25,6 +25,15 @@ inline float sqrt_lim(float R) {
     return s;
 }
 
+// The smallest float s >= 0 with fl(s + c) >= L: float addition is monotone in s, so
+// fl(s + c) < L exactly when s < add_lim(c, L). (volatile: each sum rounded to float.)
+inline float add_lim(float c, float L) {
+    volatile float s = L - c, t;
+    while (s > 0.0f && (t = s + c) >= L) s = std::nextafter((float)s, 0.0f);
+    while ((t = s + c) < L) s = std::nextafter((float)s, INFINITY);
+    return s;
+}
+
 inline void build_geom(const swarm_params_t& p, Geom& g) {
     std::memset(&g, 0, sizeof(g));
     const bool mc = p.profile == SWARM_PROFILE_STANDALONE;
@@ -237,6 +246,8 @@ inline void build_geom(const swarm_params_t& p, Geom& g) {
     g.rab_range2_hi = (float)((double)g.rab_range * g.rab_range * (1.0 + 1.0 / 1048576.0));
     g.min_dist_s_lim = sqrt_lim(g.min_dist);
     g.rab_s_lim = sqrt_lim(g.rab_range);
+    g.min_dist_pre_lim = add_lim(1e-8f, g.min_dist_s_lim);
+    g.rab_pre_lim = add_lim(1e-8f, g.rab_s_lim);
     g.inv_prox_range = 1.0f / g.prox_range;
     g.inv_unity = 1.0f / g.unity;
 }

@@ -17,3 +17,19 @@ template void launch_reset_m<SWARM_MISSION_ID>(const Geom&, const DevState&, con
 // diagnostic builds only (tools/wave_timing.py): the Homing step kernel's per-wave log
 extern "C" int swarm_debug_wave_log(void* host, size_t bytes) { return swarm::read_wave_log(host, bytes); }
 #endif
+
+#if SWARM_ARENA_PERM && SWARM_MISSION_ID == 2
+// experiment builds only (tools/arena_balance.py): the block -> arena permutation of the Homing
+// step kernel, and the per-arena costs / per-block hardware slots of its last launch
+extern "C" int swarm_debug_set_perm(const int32_t* host, size_t n) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(swarm::g_arena_perm), host, n * sizeof(int32_t), 0, hipMemcpyHostToDevice) ==
+                   hipSuccess ? 0 : -1;
+}
+extern "C" int swarm_debug_get_costs(int32_t* cost, uint32_t* hw, size_t n) {
+    if (hipMemcpyFromSymbol(cost, HIP_SYMBOL(swarm::g_arena_cost), n * sizeof(int32_t), 0, hipMemcpyDeviceToHost) !=
+        hipSuccess)
+        return -1;
+    return hipMemcpyFromSymbol(hw, HIP_SYMBOL(swarm::g_block_hw), n * sizeof(uint32_t), 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif

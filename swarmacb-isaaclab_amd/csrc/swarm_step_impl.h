@@ -38,6 +38,17 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
+// Experiment switches (timing studies; removed once measured): 1 = the variant.
+#ifndef SWARM_EXP_DISC_MASK
+#define SWARM_EXP_DISC_MASK 0
+#endif
+#ifndef SWARM_EXP_SOLVE_ROLLED
+#define SWARM_EXP_SOLVE_ROLLED 0
+#endif
+#ifndef SWARM_SEG_GROUP
+#define SWARM_SEG_GROUP 0
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -228,13 +239,14 @@ __device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t bl
 // LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
 // broadcast within an arena) and 4 float4 partial slots per thread.
 // Slot use: 0 contact-solver sums, 0-1 proximity maxima, 2-3 range-and-bearing sums.
-template <int LY>
+template <int LY, int NRED = 4>
 struct Shared {
     float2 xy[64];
     int ins[64];
-    float4 red[4][64 * ly_waves(LY)];
+    float4 red[NRED][64 * ly_waves(LY)];
     float zt[64];       // ztilde of a range-and-bearing count
     float4 face[12];    // arena faces: normal (x, y), offset -(p . n), 0
+    float4 seg[16];     // raycast segments (arena faces, internal walls): start (x, y), vector (x, y)
     float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
     int wsec[24];       // wall_sector3
 };
@@ -257,13 +269,14 @@ __device__ __forceinline__ void sync_wg() {
 
 // Per-workgroup tables staged once per launch (ztilde, arena faces, wall sectors). The first
 // read follows publish()'s exchange point, which orders it after these writes.
-template <int LY>
-__device__ __forceinline__ void stage_tables(const Geom& g, Shared<LY>& S) {
-    const int t = threadIdx.x;
+template <int LY, class SH>
+__device__ __forceinline__ void stage_tables(const Geom& g, SH& S, int t = -1) {
+    if (t < 0) t = threadIdx.x;
     if (t < 64) S.zt[t] = 1.0f - 2.0f / (1.0f + expf((float)t));   // rab_finish's expression
     if (t < 12) S.face[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_d[t], 0.0f);
     if (t < 12) S.wface[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_px[t], g.face_py[t]);
     if (t < 24) S.wsec[t] = g.wall_sector3[t];
+    if (t < 15) S.seg[t] = make_float4(g.seg_ax[t], g.seg_ay[t], g.seg_sx[t], g.seg_sy[t]);
     (void)g;
     (void)S;
     (void)t;
@@ -314,7 +327,7 @@ __device__ __forceinline__ uint32_t chunk_mask(const Lane& L, const float2* xy, 
 
 // Both observation masks of a part's chunk from one read of its C tile entries:
 // proximity discs (|d|^2 <= 0.02) and range-and-bearing candidates
-// (|d|^2 + 1e-8 < rab_range2_hi); the same tests as the two chunk_mask calls.
+// (|d|^2 + 1e-8 < rab_s_lim, evaluated exactly as |d|^2 < rab_pre_lim).
 template <int C>
 __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const float2* xy, float x, float y,
                                           uint32_t& mprox, uint32_t& mrab) {
@@ -329,7 +342,7 @@ __device__ __forceinline__ void obs_masks(const Geom& g, const Lane& L, const fl
         float dx, dy;
         const float s = sq_dist(p[jj].x, p[jj].y, x, y, dx, dy);
         a |= (ok & (s <= 0.0200f)) ? (1u << jj) : 0u;
-        b |= (ok & (s + 1e-8f < g.rab_s_lim)) ? (1u << jj) : 0u;
+        b |= (ok & (s < g.rab_pre_lim)) ? (1u << jj) : 0u;   // = s + 1e-8 < rab_s_lim (add_lim)
     }
     mprox = a;
     mrab = b;
@@ -351,8 +364,8 @@ __device__ __forceinline__ void for_each_cand(const Lane& L, const float2* xy, u
 
 // the packed 3 candidate faces of a position (wall_sector3 of its direction's 15-degree sector;
 // the angle estimate t * 45 degrees on the octant-folded ratio is within 4.1 degrees)
-template <int LY>
-__device__ __forceinline__ int wall_faces(const Shared<LY>& S, float x, float y) {
+template <int LY, class SH>
+__device__ __forceinline__ int wall_faces(const SH& S, float x, float y) {
     const float ax = fabsf(x), ay = fabsf(y);
     const float mn = fminf(ax, ay), mx = fmaxf(ax, ay);
     const float t = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;
@@ -369,8 +382,8 @@ __device__ __forceinline__ int wall_faces(const Shared<LY>& S, float x, float y)
 // add pen = 0 (a +-0 term leaves the sum bitwise unchanged), so the sum is the reference's
 // face-order sum. The wave skips the faces altogether when no robot is within the clearance of
 // the inscribed circle's rim.
-template <int LY>
-__device__ __forceinline__ void walls_dg_near(const Geom& g, const Shared<LY>& S, int faces, float& x, float& y) {
+template <int LY, class SH>
+__device__ __forceinline__ void walls_dg_near(const Geom& g, const SH& S, int faces, float& x, float& y) {
     if (SWARM_ABLATE & 8) return;
     float tx = 0.0f, ty = 0.0f;
     if (__any(fmaf(x, x, y * y) >= g.wall_safe_r2)) {
@@ -405,8 +418,8 @@ __device__ __forceinline__ void walls_mc(const Geom& g, float& x, float& y) {
 // Each wave sums its neighbour chunk; the W partial sums are added in wave order.
 // Returns false only when it is known (wave-uniformly) that no pair term
 // contributed, i.e. the push was the identity map on every lane.
-template <int LY, int C>
-__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y) {
+template <int LY, int C, class SH>
+__device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, SH& S, float& x, float& y) {
     if (SWARM_ABLATE & 4) return false;
     SWARM_WT(L.wt_push++);
     SWARM_PH_T(wt_t);
@@ -439,9 +452,10 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, Shared
     };
     if constexpr (C > 0) {
         // d = p_j - p_i here; the squared distance is sign-free and bit-identical
+        // s + 1e-8 < min_dist_s_lim as the exact test s < min_dist_pre_lim (swarm_geom_build.h add_lim)
         const uint32_t cand = chunk_mask<C>(L, S.xy, x, y, [&](float px, float py) {
             float dx, dy;
-            return sq_dist(px, py, x, y, dx, dy) + 1e-8f < g.min_dist_s_lim;
+            return sq_dist(px, py, x, y, dx, dy) < g.min_dist_pre_lim;
         }, true);
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
@@ -613,8 +627,8 @@ __device__ __forceinline__ void capsules(const Geom& g, float& x, float& y, bool
 }
 
 // DG:874-896 — pre pass, solver iterations, post pass.
-template <int MISSION, int LY, int C, bool APPLY>
-__device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& S, float& x, float& y, float qx,
+template <int MISSION, int LY, int C, bool APPLY, class SH>
+__device__ __forceinline__ void solve(const Geom& g, const Lane& L, SH& S, float& x, float& y, float qx,
                                       float qy) {
     // Both contact sequences of the Isaac profile as one fully unrolled loop
     // (straight-line code measured faster than a rolled loop here):
@@ -633,7 +647,11 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, Shared<LY>& 
     gate_walls<MISSION, ISAAC>(g, x, y);
     constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
     bool fixed = false;                                   // wave-uniform
+#if SWARM_EXP_SOLVE_ROLLED
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
     for (int it = 0; it <= K; ++it) {
         if (fixed && it < K) continue;
         const float bx = x, by = y;
@@ -713,10 +731,25 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // ES:85-142, 184-293: per-ray readings (max over segments and robot discs).
 // Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
-template <int LY, int C>
-__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const Shared<LY>& S, float x, float y,
-                                                  const float rdx[8], const float rdy[8], float prox[8],
-                                                  const uint32_t* disc_cand = nullptr) {
+// RAYS_FROM_YAW: each use evaluates ray k's world direction from (syw, cyw) (the same expression
+// as observe()'s rdx / rdy, so the same values) instead of holding 16 registers through the pass.
+template <int LY, int C, class SH, bool RAYS_FROM_YAW = false>
+__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const SH& S, float x, float y,
+                                                  const float rdx_[8], const float rdy_[8], float prox[8],
+                                                  const uint32_t* disc_cand = nullptr, float syw = 0.0f,
+                                                  float cyw = 0.0f) {
+    // (cw, sw): (cyw, syw) laundered through an empty asm at each use site, so that the compiler does
+    // not hoist the 16 ray directions out of the loops (which is what holding them would cost)
+    float cw = cyw, sw = syw;
+    auto launder = [&]() {
+        if constexpr (RAYS_FROM_YAW) {
+            cw = cyw;
+            sw = syw;
+            __asm__ volatile("" : "+v"(cw), "+v"(sw));
+        }
+    };
+    auto rdx = [&](int k) { return RAYS_FROM_YAW ? g.cos_a[k] * cw - g.sin_a[k] * sw : rdx_[k]; };
+    auto rdy = [&](int k) { return RAYS_FROM_YAW ? g.cos_a[k] * sw + g.sin_a[k] * cw : rdy_[k]; };
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length.
@@ -760,16 +793,23 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         SWARM_WT(L.wt_seg++);
         const int s = __builtin_ctz(near_mask);
         near_mask &= near_mask - 1u;
-        const float ax = g.seg_ax[s], ay = g.seg_ay[s], sx = g.seg_sx[s], sy = g.seg_sy[s];
+        // the segment from the LDS table (per-lane index: no vector loads of the constant table)
+        const float4 sg = S.seg[s];
+        const float ax = sg.x, ay = sg.y, sx = sg.z, sy = sg.w;
+        launder();
         const float qx = ax - x, qy = ay - y;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const float den = rdx[k] * sy - rdy[k] * sx;
+#if SWARM_SEG_GROUP
+            if (k == SWARM_SEG_GROUP) __builtin_amdgcn_sched_barrier(0);
+#endif
+            const float rx = rdx(k), ry = rdy(k);
+            const float den = rx * sy - ry * sx;
             const bool valid = fabsf(den) > 1e-8f;
             const float dd = den + 1e-12f;
             const float inv = frcp(dd);
             const float t = (qx * sy - qy * sx) * inv;
-            const float u = (qx * rdy[k] - qy * rdx[k]) * inv;
+            const float u = (qx * ry - qy * rx) * inv;
             // & (not &&): every operand is computed anyway, so the test is selects, not branches
             const bool hit = valid & (t >= 0.0f) & (t <= g.prox_range) & (u >= 0.0f) & (u <= 1.0f);
             const float nr = hit ? 1.0f - t * g.inv_prox_range : 0.0f;
@@ -779,9 +819,31 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
     auto disc = [&](float dx, float dy) {
         const float dsq = dx * dx + dy * dy;
+        launder();
+#if SWARM_EXP_DISC_MASK
+        // every ray's pre-test first (8 independent chains), then the hits of the rays some lane
+        // can hit
+        float pj[8], cs[8];
+        bool pre[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const float proj = rdx[k] * dx + rdy[k] * dy;
+            pj[k] = rdx(k) * dx + rdy(k) * dy;
+            cs[k] = dsq - pj[k] * pj[k];
+            pre[k] = (pj[k] > 0.0f) & (cs[k] <= g.r2);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (!__any(pre[k])) continue;
+            const float hc = fsqrt(fmaxf(g.r2 - cs[k], 0.0f));
+            const float hd = fmaxf(pj[k] - hc, 0.0f);
+            const bool hit = pre[k] & (hd <= g.prox_range);
+            const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
+            prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
+        }
+#else
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float proj = rdx(k) * dx + rdy(k) * dy;
             const float csq = dsq - proj * proj;
             const bool pre = (proj > 0.0f) & (csq <= g.r2);
             // a disc spans at most two of the 45-degree rays: the wave skips the rest
@@ -793,6 +855,7 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
+#endif
     };
     if constexpr (C > 0) {
         const uint32_t cand = disc_cand ? *disc_cand
@@ -878,7 +941,8 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
                                             float x,
                                             float y, float cyw, float syw, const float* u_replay, uint32_t purpose,
                                             uint64_t tick, float& n, float& wx, float& wy, float& axx, float& ayy,
-                                            const uint32_t* pre_cand = nullptr, const uint4* pre_rb = nullptr) {
+                                            const uint32_t* pre_cand = nullptr, const uint4* pre_rb = nullptr,
+                                            const float4* seg_tab = nullptr) {
     const bool me_in = insv[L.r] != 0;
     n = 0.0f;
     wx = 0.0f;
@@ -901,8 +965,9 @@ __device__ __forceinline__ void rab_partial(const Geom& g, const Lane& L, const 
         if (s0 < g.nseg) {
         const float rdx = dx / (dist + 1e-8f), rdy = dy / (dist + 1e-8f);
         for (int s = s0; s < g.nseg; ++s) {
-            const float sx = g.seg_sx[s], sy = g.seg_sy[s];
-            const float qx = g.seg_ax[s] - x, qy = g.seg_ay[s] - y;
+            const float4 sg = seg_tab ? seg_tab[s] : make_float4(g.seg_ax[s], g.seg_ay[s], g.seg_sx[s], g.seg_sy[s]);
+            const float sx = sg.z, sy = sg.w;
+            const float qx = sg.x - x, qy = sg.y - y;
             const float den = rdx * sy - rdy * sx;
             const float dd = den + 1e-12f;
             const float t = (qx * sy - qy * sx) / dd;
@@ -1149,8 +1214,8 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
 // Publishes positions + "strictly inside the arena" flags (LOS shortcut).
-template <int LY>
-__device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y) {
+template <int LY, class SH>
+__device__ __forceinline__ void publish(const Geom& g, const Lane& L, SH& S, float x, float y) {
     bool ins = true;
     // |p| < apothem - 1e-3 - margin implies every face is > 1e-3 away; the flag
     // only selects a shortcut (a robot flagged "not inside" gets the full,
@@ -1170,8 +1235,8 @@ __device__ __forceinline__ void publish(const Geom& g, const Lane& L, Shared<LY>
 // Range-and-bearing sums over all neighbours: this wave's chunk + the other
 // waves' partials (slots 2-3), added in wave order. Must follow publish().
 // With `with_prox`, also max-combines the proximity readings (slots 0-1).
-template <int LY, int C>
-__device__ __forceinline__ void combine(const Lane& L, Shared<LY>& S, bool with_prox, float prox[8], float& n,
+template <int LY, int C, class SH>
+__device__ __forceinline__ void combine(const Lane& L, SH& S, bool with_prox, float prox[8], float& n,
                                         float& wx, float& wy, float& axx, float& ayy) {
     if constexpr (ly_parts(LY) > 1) {
         constexpr int P = ly_parts(LY);
@@ -1223,8 +1288,8 @@ __device__ __forceinline__ void combine(const Lane& L, Shared<LY>& S, bool with_
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE, int LY, int C>
-__device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float yaw,
+template <int MISSION, int PROFILE, int LY, int C, class SH, bool EARLY_RNG = true, bool RAYS_FROM_YAW = false>
+__device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw, bool need_agg = true) {
     SWARM_PH_T(wt_t);
@@ -1232,10 +1297,12 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
     sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
+    if constexpr (!RAYS_FROM_YAW) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
-        rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
+        for (int k = 0; k < 8; ++k) {
+            rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
+            rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
+        }
     }
     float prox[8], lt[8], r4[4], zt;
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
@@ -1244,17 +1311,17 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
         obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
-        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+        if (EARLY_RNG && !u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
     }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr);
+        proximity_partial<LY, C, SH, RAYS_FROM_YAW>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr, syw, cyw);
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
         rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
-                       FUSE ? &mrab : nullptr, FUSE ? &rb : nullptr);
+                       FUSE ? &mrab : nullptr, (FUSE && EARLY_RNG) ? &rb : nullptr, S.seg);
     SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
@@ -1292,8 +1359,8 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, Shared<LY>
 
 // standalone dispatch bundle: only the range-and-bearing part is re-drawn; the
 // proximity/light aggregates equal those of the previous observation (same pose).
-template <int LY, int C>
-__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, Shared<LY>& S, float x, float y, float syw,
+template <int LY, int C, class SH>
+__device__ __forceinline__ void rab_only(const Geom& g, const Lane& L, SH& S, float x, float y, float syw,
                                          float cyw, const float* u_replay, uint64_t tick, float& ax, float& ay) {
     publish<LY>(g, L, S, x, y);
     float n, wx, wy;
@@ -1441,7 +1508,7 @@ __device__ __forceinline__ Lane make_lane(const Geom& g, int blk) {   // g: the 
     const int chunk = (L.N + P - 1) / P;
     L.j0 = L.p * chunk;
     L.j1 = min(L.N, L.j0 + chunk);
-    L.env = g.env0 + blk * apb + L.a;
+    L.env = g.env0 + SWARM_PERM_BLOCK(blk) * apb + L.a;
     L.valid = (L.a < apb) && (L.env < g.E);
     L.ab = (L.a < apb ? L.a : 0) * L.N;
     // lanes beyond the last whole arena own no robot: park their tile writes in
@@ -1655,6 +1722,171 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
         }
     }
     if constexpr (!REPLAY && ly_waves(LY) == 1) SWARM_WT_KERNEL_END(L);
+    if constexpr (!REPLAY && ly_waves(LY) == 1) SWARM_PERM_RECORD(L);
+}
+
+// ---------------------------------------------------------------------------
+//  Layout 203: the continuous-action Isaac step as a two-wave pipeline per arena
+// ---------------------------------------------------------------------------
+// A launch of layout 103 is bound by each arena's own dependent chain: one wave alone on a SIMD
+// takes ~80 % of the time four co-resident waves take (tools/heavy_alone.py), so the chip idles
+// while every wave waits on its next result. With continuous actions nothing in a substep's
+// physics reads the previous substep's observation (the wheels come from the held action, and
+// the sensor-cache aggregates are only stored after the last substep), so the two halves of a
+// substep can run side by side: wave 0 ("physics") of a 128-thread workgroup runs substep s's
+// drive, contact solver, dones, rewards and auto-reset while wave 1 ("observation") runs substep
+// s - 1's sensors and observation. Each wave keeps layout 103's lane map (3 lanes per robot) and
+// every expression of it, so the outputs are bitwise those of layout 103. Per substep the physics
+// wave hands (x, y, yaw) of its robots to the observation wave through LDS between two workgroup
+// barriers: A_s (the observation wave is done with the tile of substep s - 1) and B_s (the tile
+// of substep s is written). Measured on MI355X (Homing dandelion, tools/pipe_envs.sh): 1,024 envs
+// 31.8 vs 48.5 us per 5-substep launch, 2,048 envs 37.2 vs 50.4 us; at 4,096 envs the 8 waves per
+// SIMD it needs make it slower (59 vs 55 us), so swarm_create picks it for E <= 2 x SIMDs only.
+// Register budget: 4 waves per SIMD, i.e. all 2 E waves resident up to E = 2 x SIMDs, the range
+// swarm_create picks this layout for. (At 8 waves per SIMD, E = 4 x SIMDs, the two waves of an
+// arena need <= 64 VGPRs: with the ray directions re-evaluated per use (RAYS_FROM_YAW) and the
+// packet-loss draw late it compiles to 64 with 18 spilled, and runs 59 us against layout 103's
+// 55 us at C2 - measured)
+#ifndef SWARM_PIPE_MIN_WAVES
+#define SWARM_PIPE_MIN_WAVES 4
+#endif
+#ifndef SWARM_PIPE_EARLY_RNG
+#define SWARM_PIPE_EARLY_RNG true
+#endif
+#ifndef SWARM_PIPE_RAYS_FROM_YAW
+#define SWARM_PIPE_RAYS_FROM_YAW false
+#endif
+template <int MISSION>
+__global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
+    const Geom gr, const DevState st, const void* __restrict__ actions, const DevOut out, uint64_t tick0, int n_sub,
+    uint64_t reset_any) {
+    constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;
+    const Geom& g = kGeomTab[MISSION][PROFILE];
+    __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
+    __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
+    __shared__ float yaw_tile[64];
+    const int lane = threadIdx.x & 63;
+    const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
+    // each role builds its own lane context (separate live ranges for the two register budgets)
+    auto lane_ctx = [&]() {
+        Lane L = make_lane<NA, LY>(gr, (int)blockIdx.x);
+        L.tid = lane;                 // partial slots are per wave
+        L.pbase = lane - L.p;
+        return L;
+    };
+    if (!obs_wave) {
+        const Lane L = lane_ctx();
+        const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
+        stage_tables<LY>(g, SP, lane);
+        float x = 0.0f, y = 0.0f, yaw = 0.0f, wl = 0.0f, wr = 0.0f, ax = 0.0f, ay = 0.0f;
+        uint32_t fsm = 0;
+        int gprev = 1, flags = 0, ep_len = 0;
+        float ep_rew = 0.0f, comp = 0.0f;
+        if (L.valid) {
+            x = st.x[q];
+            y = st.y[q];
+            yaw = st.yaw[q];
+            fsm = st.fsm[q];
+            gprev = st.gprev[q];
+            flags = st.flags[q];
+            ep_len = st.ep_len[L.env];
+            ep_rew = st.ep_rew[L.env];
+            comp = st.comp_rew[L.env];
+            const float2 a = reinterpret_cast<const float2*>(actions)[q];
+            ax = a.x;
+            ay = a.y;
+        }
+        float rew_acc = 0.0f;
+        bool trunc_acc = false;
+        const DevReplay rp{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+        for (int s = 0; s < n_sub; ++s) {
+            const uint64_t tick = tick0 + (uint64_t)s;
+            const float lw = clampf(ax, -1.0f, 1.0f) * g.max_speed;                   // DG:807-809
+            const float rw = clampf(ay, -1.0f, 1.0f) * g.max_speed;
+            wl = lw;
+            wr = rw;
+            float syaw, cyaw;
+            sincosf(yaw, &syaw, &cyaw);   // layout 103 carries these from the observation of yaw
+            for (int d = 0; d < gr.decimation; ++d) {
+                const float qx = x, qy = y;
+                if (d > 0) sincosf(yaw, &syaw, &cyaw);
+                integrate(g, lw, rw, x, y, yaw, syaw, cyaw);
+                solve<MISSION, LY, C, true>(g, L, SP, x, y, qx, qy);
+            }
+            ep_len += 1;
+            const bool tout = ep_len >= gr.max_len;                                    // DG:1200-1209
+            if (tout && L.valid && L.p == 0) {
+                float c5[5];
+                critic5(g, x, y, yaw, c5);
+                float* o = st.tcrit + (size_t)q * 5;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) o[k] = c5[k];
+            }
+            const float r = team_reward<MISSION, PROFILE>(g, L, x, y, gprev, flags, tout);
+            ep_rew += r;
+            rew_acc += r;
+            if (tout) {                                                                // DG:1242-1273
+                ep_len = 0;
+                comp = ep_rew;
+                ep_rew = 0.0f;
+                if (L.valid) spawn_isaac(g, L, rp, tick, x, y, yaw);
+            }
+            if ((reset_any >> s) & 1ull)                                               // DG:1262 (all envs)
+                solve<MISSION, LY, C, false>(g, L, SP, x, y, 0.0f, 0.0f);
+            if (tout) {
+                gprev = ground_code<MISSION, PROFILE>(g, x, y);
+                fsm = 0u;
+                if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
+            }
+            trunc_acc |= tout;
+            __syncthreads();                   // A_s: the observation wave is done with substep s - 1
+            if (L.p == 0) {
+                SO.xy[L.r] = make_float2(x, y);
+                yaw_tile[L.r] = yaw;
+            }
+            __syncthreads();                   // B_s: the tile of substep s is written
+        }
+        if (L.valid && L.p == 0) {
+            st.x[q] = x;
+            st.y[q] = y;
+            st.yaw[q] = yaw;
+            st.fsm[q] = fsm;
+            st.wl[q] = wl;
+            st.wr[q] = wr;
+            st.gprev[q] = (uint8_t)gprev;
+            st.flags[q] = (uint8_t)flags;
+            if (L.i == 0) {
+                st.ep_len[L.env] = ep_len;
+                st.ep_rew[L.env] = ep_rew;
+                st.comp_rew[L.env] = comp;
+                if (out.reward) out.reward[L.env] = rew_acc;
+                if (out.trunc) out.trunc[L.env] = trunc_acc ? 1 : 0;
+            }
+        }
+    } else {
+        const Lane L = lane_ctx();
+        const uint32_t q = L.valid ? (uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i : 0u;
+        const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
+        stage_tables<LY>(g, SO, lane);
+        Agg cache = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        for (int s = 0; s < n_sub; ++s) {
+            __syncthreads();                   // A_s
+            __syncthreads();                   // B_s
+            const float2 p = SO.xy[L.r];
+            const float yaw = yaw_tile[L.r];
+            float syaw, cyaw;
+            observe<MISSION, PROFILE, LY, C, Shared<LY, 4>, SWARM_PIPE_EARLY_RNG, SWARM_PIPE_RAYS_FROM_YAW>(
+                g, L, SO, p.x, p.y, yaw, nullptr, tick0 + (uint64_t)s, out.obs, cache, syaw, cyaw, s == n_sub - 1);
+        }
+        if (L.valid && L.p == 0) {
+            st.cache[q] = cache.pv;
+            st.cache[EN + q] = cache.pa;
+            st.cache[2 * EN + q] = cache.lv;
+            st.cache[3 * EN + q] = cache.la;
+            st.cache[4 * EN + q] = cache.ax;
+            st.cache[5 * EN + q] = cache.ay;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1737,7 +1969,16 @@ static void launch_step_t(const Geom& g, const DevState& st, const void* act, co
             hipLaunchKernelGGL((step_kernel<M, P, D, NA, LY, false>), dim3(blocks), dim3(64 * ly_waves(LY)), 0,       \
                                stream, g, st, act, ovr, out, rp, tick, n_sub, reset_any);                             \
     } while (0)
-    if (g.layout == 103) {   // one arena per wave, 3 lanes per robot (N <= 21, checked by swarm_create)
+    if constexpr (P == ISAAC && !D) {
+        // layout 203: the two-wave pipeline of the continuous Isaac step (production kernel; the
+        // replay kernels of the parity tests run layout 103, whose arithmetic it shares)
+        if (g.layout == 203 && g.N == 20 && !replay && g.env0 == 0 && (g.env_n == 0 || g.env_n == g.E)) {
+            hipLaunchKernelGGL((step_kernel_pipe<M>), dim3(g.E), dim3(128), 0, stream, g, st, act, out, tick, n_sub,
+                               reset_any);
+            return;
+        }
+    }
+    if (g.layout == 103 || g.layout == 203) {   // one arena per wave, 3 lanes per robot (N <= 21, checked by swarm_create)
         const int blocks = g.env_n > 0 ? g.env_n : g.E;   // arenas [env0, env0 + blocks)
         if (g.N == 20)
             SWARM_LAUNCH_STEP(20, 103);

@@ -47,7 +47,7 @@ def _params(**kw):
 @pytest.mark.parametrize("bad", [dict(abi_version=1), dict(mission=9), dict(profile=3), dict(num_envs=0),
                                  dict(num_agents=65), dict(num_agents=0), dict(obs_dim=7),
                                  dict(max_episode_length=0), dict(env_offset=-1), dict(layout=3), dict(layout=2), dict(layout=1), dict(num_envs=5_000_000),
-                                 dict(layout=103, num_agents=22)])
+                                 dict(layout=103, num_agents=22), dict(layout=203, num_agents=22)])
 def test_create_rejects_bad_params(bad):
     lib = _native.load()
     h = C.c_void_p()

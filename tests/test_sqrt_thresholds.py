@@ -33,3 +33,31 @@ def test_squared_threshold_is_the_sqrt_decision():
         s = (rng.uniform(0, 2 * R * R, 200_000)).astype(f32)
         t = (s + f32(1e-8)).astype(f32)
         np.testing.assert_array_equal(f32(R) - np.sqrt(t) > 0, t < lim)
+
+
+def add_lim(c, L):
+    """Restatement of swarm_geom_build.h add_lim: the smallest float32 s >= 0 with fl(s + c) >= L."""
+    c, L = f32(c), f32(L)
+    s = f32(L - c)
+    while s > 0 and f32(s + c) >= L:
+        s = np.nextafter(s, f32(0))
+    while f32(s + c) < L:
+        s = np.nextafter(s, f32(np.inf))
+    return s
+
+
+def test_pre_add_threshold_is_the_same_decision():
+    """The candidate masks compare s = |d|^2 itself with x_pre_lim = add_lim(1e-8, x_s_lim) instead of
+    adding the reference's 1e-8 first (DG:1088 dist = sqrt(dx^2 + dy^2 + 1e-8), ES:411): the same
+    decision for every float32 s, as float addition is monotone."""
+    rng = np.random.default_rng(5)
+    for R in (0.07, 0.6):
+        lim = sqrt_lim(R)
+        pre = add_lim(1e-8, lim)
+        bits = pre.view(np.int32) + np.arange(-8192, 8193, dtype=np.int32)
+        s = bits.view(np.float32)
+        np.testing.assert_array_equal((s + f32(1e-8)).astype(f32) < lim, s < pre)
+        s = rng.uniform(0, 2 * R * R, 500_000).astype(f32)
+        np.testing.assert_array_equal((s + f32(1e-8)).astype(f32) < lim, s < pre)
+        # and end to end against the reference's sqrt decision
+        np.testing.assert_array_equal(f32(R) - np.sqrt((s + f32(1e-8)).astype(f32)) > 0, s < pre)
