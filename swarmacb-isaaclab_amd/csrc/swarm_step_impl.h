@@ -38,17 +38,6 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
-// Experiment switches (timing studies; removed once measured): 1 = the variant.
-#ifndef SWARM_EXP_DISC_MASK
-#define SWARM_EXP_DISC_MASK 0
-#endif
-#ifndef SWARM_EXP_SOLVE_ROLLED
-#define SWARM_EXP_SOLVE_ROLLED 0
-#endif
-#ifndef SWARM_SEG_GROUP
-#define SWARM_SEG_GROUP 0
-#endif
-
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -647,11 +636,7 @@ __device__ __forceinline__ void solve(const Geom& g, const Lane& L, SH& S, float
     gate_walls<MISSION, ISAAC>(g, x, y);
     constexpr int K = apply ? 5 : 4;                      // collision_solver_iterations (DGC:127) + 1
     bool fixed = false;                                   // wave-uniform
-#if SWARM_EXP_SOLVE_ROLLED
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
     for (int it = 0; it <= K; ++it) {
         if (fixed && it < K) continue;
         const float bx = x, by = y;
@@ -731,25 +716,10 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // ES:85-142, 184-293: per-ray readings (max over segments and robot discs).
 // Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
-// RAYS_FROM_YAW: each use evaluates ray k's world direction from (syw, cyw) (the same expression
-// as observe()'s rdx / rdy, so the same values) instead of holding 16 registers through the pass.
-template <int LY, int C, class SH, bool RAYS_FROM_YAW = false>
+template <int LY, int C, class SH>
 __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const SH& S, float x, float y,
-                                                  const float rdx_[8], const float rdy_[8], float prox[8],
-                                                  const uint32_t* disc_cand = nullptr, float syw = 0.0f,
-                                                  float cyw = 0.0f) {
-    // (cw, sw): (cyw, syw) laundered through an empty asm at each use site, so that the compiler does
-    // not hoist the 16 ray directions out of the loops (which is what holding them would cost)
-    float cw = cyw, sw = syw;
-    auto launder = [&]() {
-        if constexpr (RAYS_FROM_YAW) {
-            cw = cyw;
-            sw = syw;
-            __asm__ volatile("" : "+v"(cw), "+v"(sw));
-        }
-    };
-    auto rdx = [&](int k) { return RAYS_FROM_YAW ? g.cos_a[k] * cw - g.sin_a[k] * sw : rdx_[k]; };
-    auto rdy = [&](int k) { return RAYS_FROM_YAW ? g.cos_a[k] * sw + g.sin_a[k] * cw : rdy_[k]; };
+                                                  const float rdx[8], const float rdy[8], float prox[8],
+                                                  const uint32_t* disc_cand = nullptr) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length.
@@ -796,14 +766,10 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         // the segment from the LDS table (per-lane index: no vector loads of the constant table)
         const float4 sg = S.seg[s];
         const float ax = sg.x, ay = sg.y, sx = sg.z, sy = sg.w;
-        launder();
         const float qx = ax - x, qy = ay - y;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-#if SWARM_SEG_GROUP
-            if (k == SWARM_SEG_GROUP) __builtin_amdgcn_sched_barrier(0);
-#endif
-            const float rx = rdx(k), ry = rdy(k);
+            const float rx = rdx[k], ry = rdy[k];
             const float den = rx * sy - ry * sx;
             const bool valid = fabsf(den) > 1e-8f;
             const float dd = den + 1e-12f;
@@ -819,31 +785,9 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
     auto disc = [&](float dx, float dy) {
         const float dsq = dx * dx + dy * dy;
-        launder();
-#if SWARM_EXP_DISC_MASK
-        // every ray's pre-test first (8 independent chains), then the hits of the rays some lane
-        // can hit
-        float pj[8], cs[8];
-        bool pre[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            pj[k] = rdx(k) * dx + rdy(k) * dy;
-            cs[k] = dsq - pj[k] * pj[k];
-            pre[k] = (pj[k] > 0.0f) & (cs[k] <= g.r2);
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (!__any(pre[k])) continue;
-            const float hc = fsqrt(fmaxf(g.r2 - cs[k], 0.0f));
-            const float hd = fmaxf(pj[k] - hc, 0.0f);
-            const bool hit = pre[k] & (hd <= g.prox_range);
-            const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
-            prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
-        }
-#else
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float proj = rdx(k) * dx + rdy(k) * dy;
+            const float proj = rdx[k] * dx + rdy[k] * dy;
             const float csq = dsq - proj * proj;
             const bool pre = (proj > 0.0f) & (csq <= g.r2);
             // a disc spans at most two of the 45-degree rays: the wave skips the rest
@@ -855,7 +799,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
             const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
             prox[k] = fmaxf(prox[k], hit ? rv : 0.0f);
         }
-#endif
     };
     if constexpr (C > 0) {
         const uint32_t cand = disc_cand ? *disc_cand
@@ -1288,7 +1231,7 @@ __device__ __forceinline__ void combine(const Lane& L, SH& S, bool with_prox, fl
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE, int LY, int C, class SH, bool EARLY_RNG = true, bool RAYS_FROM_YAW = false>
+template <int MISSION, int PROFILE, int LY, int C, class SH>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw, bool need_agg = true) {
@@ -1297,12 +1240,10 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, flo
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
     sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
-    if constexpr (!RAYS_FROM_YAW) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
-            rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
-        }
+    for (int k = 0; k < 8; ++k) {
+        rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
+        rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
     }
     float prox[8], lt[8], r4[4], zt;
     float n = 0.0f, wx = 0.0f, wy = 0.0f, axx = 0.0f, ayy = 0.0f;
@@ -1311,17 +1252,17 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, flo
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
         obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
-        if (EARLY_RNG && !u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
     }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<LY, C, SH, RAYS_FROM_YAW>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr, syw, cyw);
+        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr);
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
         rab_partial<C>(g, L, S.xy, S.ins, x, y, cyw, syw, u_replay, RNG_RAB_OBS, tick, n, wx, wy, axx, ayy,
-                       FUSE ? &mrab : nullptr, (FUSE && EARLY_RNG) ? &rb : nullptr, S.seg);
+                       FUSE ? &mrab : nullptr, FUSE ? &rb : nullptr, S.seg);
     SWARM_PH_NEXT(L, PH_RAB, wt_t);
     combine<LY, C>(L, S, true, prox, n, wx, wy, axx, ayy);
     SWARM_PH_NEXT(L, PH_COMBINE, wt_t);
@@ -1744,20 +1685,11 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // SIMD it needs make it slower (59 vs 55 us), so swarm_create picks it for E <= 2 x SIMDs only.
 // Register budget: 4 waves per SIMD, i.e. all 2 E waves resident up to E = 2 x SIMDs, the range
 // swarm_create picks this layout for. (At 8 waves per SIMD, E = 4 x SIMDs, the two waves of an
-// arena need <= 64 VGPRs: with the ray directions re-evaluated per use (RAYS_FROM_YAW) and the
-// packet-loss draw late it compiles to 64 with 18 spilled, and runs 59 us against layout 103's
-// 55 us at C2 - measured)
-#ifndef SWARM_PIPE_MIN_WAVES
-#define SWARM_PIPE_MIN_WAVES 4
-#endif
-#ifndef SWARM_PIPE_EARLY_RNG
-#define SWARM_PIPE_EARLY_RNG true
-#endif
-#ifndef SWARM_PIPE_RAYS_FROM_YAW
-#define SWARM_PIPE_RAYS_FROM_YAW false
-#endif
+// arena must fit 64 VGPRs: with the ray directions re-evaluated per use and the packet-loss draw
+// late it compiled to 64 with 18 spilled and ran 59 us against layout 103's 55 us at C2 - measured,
+// DESIGN.md §13; the variant is in git history.)
 template <int MISSION>
-__global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
+__global__ __launch_bounds__(128, 4) void step_kernel_pipe(
     const Geom gr, const DevState st, const void* __restrict__ actions, const DevOut out, uint64_t tick0, int n_sub,
     uint64_t reset_any) {
     constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;
@@ -1875,8 +1807,8 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             const float2 p = SO.xy[L.r];
             const float yaw = yaw_tile[L.r];
             float syaw, cyaw;
-            observe<MISSION, PROFILE, LY, C, Shared<LY, 4>, SWARM_PIPE_EARLY_RNG, SWARM_PIPE_RAYS_FROM_YAW>(
-                g, L, SO, p.x, p.y, yaw, nullptr, tick0 + (uint64_t)s, out.obs, cache, syaw, cyaw, s == n_sub - 1);
+            observe<MISSION, PROFILE, LY, C>(g, L, SO, p.x, p.y, yaw, nullptr, tick0 + (uint64_t)s, out.obs, cache, syaw,
+                                             cyaw, s == n_sub - 1);
         }
         if (L.valid && L.p == 0) {
             st.cache[q] = cache.pv;
