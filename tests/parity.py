@@ -140,6 +140,8 @@ def reference_after(fx, t: int) -> dict:
     return ref
 
 
+# FROZEN since round 4: the envelope is defined by exactly this set, in this order (the order of
+# the "@outs" outcome tuples, which `reproduced_by` names); tests/test_parity_rule.py pins it.
 PERTURBATIONS = ("yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-", "sin+", "sin-", "cos+", "cos-", "sc+-", "sc-+")
 # libm nudges per perturbation: (sin, cos, atan2 / exp) ulps
 _LIBM = {"lm+": (1, 1, 1), "lm-": (-1, -1, -1), "sin+": (1, 0, 0), "sin-": (-1, 0, 0), "cos+": (0, 1, 0),
@@ -227,6 +229,27 @@ def _near_outcome(key: str, v, spread: dict, plain) -> np.ndarray:
     return ok
 
 
+def reproduced_by(key: str, v, spread: dict, idx: tuple) -> list[str]:
+    """The oracle runs whose output at element idx is within the plain 1e-5 bar of v:
+    "plain" (unperturbed) and/or PERTURBATIONS names, in that order."""
+    b = float(np.asarray(spread[key + "@base"])[idx])
+    off = float(_signed(key, np.asarray(v, np.float64)[idx], b))
+    plain = RTOL * float(np.asarray(_scale(key, np.asarray(spread[key + "@base"])))[idx])
+    wrap = _angle_mask(key, np.shape(spread[key + "@base"])) is not None
+
+    def near(o):
+        d = abs(off - o)
+        if wrap:
+            d = min(d, abs(d - TWO_PI))
+        return d <= plain
+
+    names = ["plain"] if near(0.0) else []
+    outs = spread.get(key + "@outs", ())
+    assert len(outs) in (0, len(PERTURBATIONS)), "outcome tuple out of step with PERTURBATIONS"
+    names += [p for p, o in zip(PERTURBATIONS, outs) if near(float(np.asarray(o)[idx]))]
+    return names
+
+
 def float_verdict(key: str, g, r, spread: dict | None):
     """(ok, plain_ok, hull_only) element masks of the fp32 rule in the module docstring."""
     d = _delta(key, g, r)
@@ -303,7 +326,10 @@ def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = 
                     stats["hull_examples"].append(
                         {"key": k, "index": list(idx), "got": float(g[idx]), "ref": float(r[idx]),
                          "hull": [float(b + spread[k + "@lo"][idx]), float(b + spread[k + "@hi"][idx])],
-                         "spread": float(sp[idx])})
+                         "spread": float(sp[idx]),
+                         "rule": "membership" if float(sp[idx]) > SPREAD_CAP else "prox_vector",
+                         "got_reproduced_by": reproduced_by(k, g, spread, idx),
+                         "ref_reproduced_by": reproduced_by(k, r, spread, idx)})
             if bad.any():
                 idx = tuple(np.argwhere(bad)[0])
                 tol = tolerance(k, r, spread.get(k, 0.0))

@@ -41,3 +41,22 @@ def test_outcomes_follow_env_subsets():
     sub = P._take_envs(sp, np.array([0, 2]), {})
     assert len(sub["obs@outs"]) == 2 and sub["obs@outs"][0].shape == (2, 2)
     np.testing.assert_array_equal(sub["obs@outs"][0], np.eye(4, 2)[[0, 2]])
+
+
+def test_perturbation_set_is_frozen():
+    # the envelope's definition: changing it needs a new record, not a silent edit
+    assert P.PERTURBATIONS == ("yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-", "sin+", "sin-", "cos+", "cos-",
+                               "sc+-", "sc-+")
+
+
+def test_hull_examples_name_the_perturbation_that_reproduces_them():
+    base = np.zeros(2)
+    outs = [np.zeros(2)] * len(P.PERTURBATIONS)
+    outs[5] = np.array([0.3937, 0.0])                      # "lm-" reaches the far side of the jump
+    sp = _spread(base, outs)
+    stats = {}
+    errs = P.compare({"obs": np.array([0.3937, 0.0], np.float32)}, {"obs": np.zeros(2, np.float32)}, sp,
+                     stats=stats)
+    assert not errs and stats["hull_elements"] == 1
+    ex, = stats["hull_examples"]
+    assert ex["got_reproduced_by"] == ["lm-"] and ex["ref_reproduced_by"][0] == "plain"

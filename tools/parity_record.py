@@ -31,6 +31,12 @@ def main(src: str, dst: str, note: str = ""):
                 g["hull_examples"] += [dict(e, test=r["test"]) for e in v][:max(0, 16 - len(g["hull_examples"]))]
             else:
                 g[k] = g.get(k, 0) + v
+    # which perturbed oracle run reproduces each hull element's GPU value (membership rule)
+    by_pert: dict = {}
+    for r in rows:
+        for e in r.get("hull_examples", []):
+            for name in e.get("got_reproduced_by", []) or ["(vector rule)"]:
+                by_pert[name] = by_pert.get(name, 0) + 1
     rec = {
         "source": note or f"pytest -m gpu on MI355X (tests/parity.py record_stats), {src}",
         "rule": ("discrete outputs exact unless a 1-ulp input perturbation flips them; fp32 |got-ref| <= "
@@ -39,6 +45,9 @@ def main(src: str, dst: str, note: str = ""):
                  "of the oracle's own outputs (unperturbed, or under one of the 1-ulp input / libm "
                  "perturbations: yaw, positions, all libm results, sin / cos alone or opposed); the "
                  "proximity aggregate angle may pass as a vector (8e-5); angles mod 2 pi"),
+        "perturbations": ["yaw+", "yaw-", "pos+", "pos-", "lm+", "lm-", "sin+", "sin-", "cos+", "cos-",
+                          "sc+-", "sc-+"],
+        "hull_got_reproduced_by": by_pert,
         "groups": groups,
         "per_test": rows,
     }
