@@ -31,7 +31,9 @@
 #include "swarm_launch.h"
 
 // Timing-only ablation switches (tools/critic_ablate.sh; results are WRONG by
-// design): 1 logits, 2 softmax, 4 P.V, 8 fc_out MFMA, 16 LayerNorm + pooling.
+// design): 1 logits, 2 softmax, 4 P.V (rsa_baselines_kernel: the head products),
+// 8 fc_out MFMA (rsa_baselines_kernel: the VW projection), 16 LayerNorm + pooling,
+// 32 (rsa_baselines_kernel) the residual loads.
 #ifndef RSA_ABLATE
 #define RSA_ABLATE 0
 #endif
@@ -41,22 +43,6 @@
 #ifndef RSA_SHARED_VW
 #define RSA_SHARED_VW 1
 #endif
-#ifndef RSA_P_WIDE
-#define RSA_P_WIDE 1
-#endif
-#ifndef RSA_GEMM_SCHED_BARRIER
-#define RSA_GEMM_SCHED_BARRIER 1
-#endif
-// 1: rsa_baselines_kernel issues a head's projected-value MFMAs, then runs that head's softmax
-// on the VALU while they are in flight, and only then stores their results (the two are
-// independent); 0: projected values stored first, softmax after. Measured at C3 (8192 envs,
-// tools/critic_ablate.py, identical outputs): 1.58 ms with the overlap vs 1.48 ms without (the
-// three live accumulator chains and the softmax's registers serialise worse than the stores),
-// so 0 is the default.
-#ifndef RSA_VW_OVERLAP
-#define RSA_VW_OVERLAP 0
-#endif
-
 namespace {
 
 constexpr int HD = 128;           // embedding width (critic hidden_units of the cyclamen / tulip / OC configs)
@@ -348,121 +334,163 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
 // (N*N) x N x 128 product per head over the action rows they share; the state
 // row of set s (its own member 0) adds a rank-1 term on the VALU. That replaces
 // the per-set P.V and the (N*N) x 128 x 128 fc_out: 5056 instead of 8288
-// 16x16x4 MFMAs per env at 4 heads. The 400 x 128 outputs of an env stay in
-// VGPRs (25 row tiles of 16 per wave, each wave one 16-column tile) across the
-// heads; bias, residual, LayerNorm and the set means then run per group of 4
-// sets through LDS as in rsa_pool_kernel. Summation order differs from the
+// 16x16x4 MFMAs per env at 4 heads. Summation order differs from the
 // reference's (fp32 reassociation, ~1e-6 relative).
+//
+// Sixteen waves in two roles (four per SIMD), walking an env's sets in groups of 4
+// (80 set rows = 5 row tiles):
+//   product waves 0-7 own output columns 16w .. 16w + 15. Per env they project
+//     their columns of VW_h for every head (the action rows' B fragments stay in
+//     VGPRs, the state rows in a wave-private LDS slab); per group and row tile
+//     they run all heads' MFMAs into one accumulator (NH x 5 MFMAs), add the
+//     state rows' rank-1 terms, bias and residual, and write the group's rows;
+//   softmax waves 8-15 compute the NEXT group's probabilities (every head) into
+//     the other of two P buffers meanwhile, so the VALU softmax issues on the
+//     SIMDs beside the matrix-core chains instead of between them;
+//   all 16 then run the group's LayerNorm statistics and set means.
+// P is stored as the product waves' A fragments: for head h, row tile t of the
+// group and lane (cl, kq), the actions 5 kq .. 5 kq + 4 of row 16 t + cl as one
+// float4 and one float (one b128 + one b32 read, lane-contiguous).
+// Workgroup barrier that orders LDS only: global loads stay in flight across it (the
+// kernel shares nothing through global memory between its waves).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Study build (-DRSA_TRACE=1, tools/critic_trace.py): every wave of blocks 0-3 stamps the shader
+// clock on arriving at and leaving each barrier, for its 5th-8th envs.
+#ifndef RSA_TRACE
+#define RSA_TRACE 0
+#endif
+#if RSA_TRACE
+constexpr int RSA_TRACE_STAMPS = 40;
+__device__ unsigned long long g_rsa_trace[4 * 4 * 16 * RSA_TRACE_STAMPS];
+#define RSA_BAR(k)                                                                                   \
+    do {                                                                                             \
+        const int it_ = (e - (int)blockIdx.x) / (int)gridDim.x - 4;                                  \
+        const bool on_ = blockIdx.x < 4 && it_ >= 0 && it_ < 4 && lane == 0;                         \
+        unsigned long long* tr_ = &g_rsa_trace[((blockIdx.x * 4 + it_) * 16 + w) * RSA_TRACE_STAMPS]; \
+        if (on_) tr_[2 * (k)] = __builtin_amdgcn_s_memtime();                                        \
+        lds_barrier();                                                                               \
+        if (on_) tr_[2 * (k) + 1] = __builtin_amdgcn_s_memtime();                                    \
+    } while (0)
+#define RSA_STAMP(k)                                                                                 \
+    do {                                                                                             \
+        const int it_ = (e - (int)blockIdx.x) / (int)gridDim.x - 4;                                  \
+        if (blockIdx.x < 4 && it_ >= 0 && it_ < 4 && lane == 0)                                      \
+            g_rsa_trace[((blockIdx.x * 4 + it_) * 16 + w) * RSA_TRACE_STAMPS + (k)] =                \
+                __builtin_amdgcn_s_memtime();                                                        \
+    } while (0)
+#else
+#define RSA_BAR(k) lds_barrier()
+#define RSA_STAMP(k) do {} while (0)
+#endif
+
+constexpr int NTB = 1024;                // 16 waves
+constexpr int MW = 8;                    // product waves
+constexpr int GR = SETS * NMAX;          // set rows per group (80)
+constexpr int GT = GR / 16;              // row tiles per group (5)
+
 template <int NH>
-__global__ void __launch_bounds__(NT) rsa_baselines_kernel(int B, const float* __restrict__ X,
-                                                            const float* __restrict__ QKV,
-                                                            const float* __restrict__ Wo,
-                                                            const float* __restrict__ bo, float* __restrict__ pooled) {
+__global__ void __launch_bounds__(NTB) rsa_baselines_kernel(int B, const float* __restrict__ X,
+                                                             const float* __restrict__ QKV,
+                                                             const float* __restrict__ Wo,
+                                                             const float* __restrict__ bo, float* __restrict__ pooled) {
     constexpr int N = NMAX;                 // 20 entities per set, 20 sets per env
     constexpr int R = 2 * N;                // entity rows per env
     constexpr int DH = HD / NH;
-    constexpr int ROWS = N * N;             // set rows per env
-    constexpr int TILES = ROWS / 16;        // 25 row tiles of 16
-#if RSA_P_WIDE
-    // P row: lane group kq's five k-steps (actions 5 kq .. 5 kq + 4) at 8 kq, so a lane reads
-    // them as one b128 + one b32; stride 36: the b128 reads of 16 lanes cover 64 banks
-    constexpr int PS = 36;
-    constexpr int PG = 8;
-#else
-    constexpr int PS = N;                   // P row stride: rows 16 B aligned; the A-fragment reads
-                                            // (20 cl + 5 kq) hit 64 distinct banks
-    constexpr int PG = N / 4;
-#endif
-    constexpr int SH = R * SW + 4;          // logit plane stride (16 B aligned rows for float4 reads)
-    constexpr int GROUPS = N / SETS;        // 5 groups of 4 sets in the epilogue
-    static_assert(ROWS % 16 == 0 && N % 4 == 0 && N % SETS == 0, "N = 20 layout");
+    constexpr int SWB = R;                  // logit row stride (unpadded: LDS budget)
+    constexpr int SHB = R * SWB;            // logit plane per head
+    constexpr int GROUPS = N / SETS;        // 5 groups of 4 sets
+    constexpr int PH = GT * 64 * 5 + GR;    // one head's P of a group: fragments (float4 | float) + P0
+    constexpr int PB = NH * PH;             // one P buffer
+    constexpr int SOFT = NTB - MW * 64;     // softmax lanes
+    static_assert(N % 4 == 0 && N % SETS == 0 && N / 4 == 5 && GR % 16 == 0, "N = 20 layout");
+    static_assert(PB % 4 == 0 && (GT * 64 * 5) % 4 == 0, "P buffers 16 B aligned");
+    static_assert(NH * GR <= SOFT, "one softmax pass per group");
 
-    __shared__ __attribute__((aligned(16))) float Xs[R * LDSW];
-    __shared__ __attribute__((aligned(16))) float Vs[R * LDSW];
-    __shared__ __attribute__((aligned(16))) float S[NH * SH];
-    // union: Q | K rows (logits), then one head's VW rows + P + P0, then the epilogue rows + stats
+    __shared__ __attribute__((aligned(16))) float S[NH * SHB];
+    __shared__ __attribute__((aligned(16))) float VWS[MW * NH * N * 16];   // [wave][h][state row][col]
+    __shared__ __attribute__((aligned(16))) float Pb[2 * PB];
+    // union: Q | K rows (logits), the VW hand-over tile, then the group's rows + stats
     constexpr int U_QK = 2 * R * LDSW;
-    constexpr int U_HEAD = R * LDSW + ROWS * PS + ROWS;
-    constexpr int U_EPI = SETS * N * LDSW + SETS * 2 * N;
-    constexpr int U = U_QK > U_HEAD ? (U_QK > U_EPI ? U_QK : U_EPI) : (U_HEAD > U_EPI ? U_HEAD : U_EPI);
+    constexpr int U_EPI = GR * LDSW + SETS * 2 * N;
+    constexpr int U = U_QK > U_EPI ? U_QK : U_EPI;
+    static_assert(MW * N * 16 <= U, "VW hand-over tile");
+    // at 4 heads (the LDS budget) the V rows live in P buffer 1 until group 1's softmax
+    constexpr bool V_ALIAS = R * LDSW <= PB;
+    __shared__ __attribute__((aligned(16))) float Vsep[V_ALIAS ? 4 : R * LDSW];
     __shared__ __attribute__((aligned(16))) float Us[U];
     float* Qs = Us;
     float* Ks = Us + R * LDSW;
-    float* VW = Us;                          // [R][LDSW]: this head's V_h W_o,h^T rows
-    float* P = Us + R * LDSW;                // [ROWS][PS]: P[set row][action j] (0 at j = s)
-    float* P0 = P + ROWS * PS;               // [ROWS]: weight of the set's own state row
-    float* PF = Us;                          // [SETS * N][LDSW]: epilogue rows of a group
-    float* stats = Us + SETS * N * LDSW;     // [SETS][2N]
+    float* Vs = V_ALIAS ? Pb + PB : Vsep;
+    float* PF = Us;                          // [GR][LDSW]: the group's rows
+    float* stats = Us + GR * LDSW;           // [SETS][2N]
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int w = tid >> 6;                  // wave: owns output columns 16w .. 16w + 15
+    const int w = tid >> 6;
+    const bool prod = w < MW;
     const int cl = lane & 15, kq = lane >> 4;
-    const int col = 16 * w + cl;
+    const int col = 16 * (w & (MW - 1)) + cl;           // product waves' output column
+    // product wave w's state rows of VW: VWS[((w * NH + h) * N + row) * 16 + col - 16 w]; its
+    // hand-over tile of VW_h's action rows: Us[(w * N + row - N) * 16 + col - 16 w]
 
     const float bias = bo[col];
     const float sqrt_d = 11.313708498984761f;
 
     for (int e = blockIdx.x; e < B; e += gridDim.x) {
         // An opaque zero per env: row and member indices derived from it are recomputed
-        // in the loop instead of being hoisted as hundreds of loop-invariant registers
-        // (which spill next to the 100 accumulator registers).
+        // in the loop instead of being hoisted as loop-invariant registers.
         int z;
         asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-        // ---- phase 0: x, q, k, v of the env's 2N entity rows
-        const float4* x4 = reinterpret_cast<const float4*>(X + (size_t)e * R * HD);
+        const float* xe = X + (size_t)e * R * HD;
+        // ---- phase 0: q, k, v of the env's 2N entity rows
         const float4* q4 = reinterpret_cast<const float4*>(QKV + (size_t)e * R * 3 * HD);
-        for (int i = tid; i < R * (HD / 4); i += NT) {
-            const int r = i / (HD / 4), c4 = i % (HD / 4);
-            *reinterpret_cast<float4*>(&Xs[r * LDSW + 4 * c4]) = x4[i];
-        }
-        for (int i = tid; i < R * (3 * HD / 4); i += NT) {
+        for (int i = tid; i < R * (3 * HD / 4); i += NTB) {
             const int r = i / (3 * HD / 4), c4 = i % (3 * HD / 4), c = 4 * c4;
             float* dst = c < HD ? &Qs[r * LDSW + c] : c < 2 * HD ? &Ks[r * LDSW + c - HD] : &Vs[r * LDSW + c - 2 * HD];
             *reinterpret_cast<float4*>(dst) = q4[i];
         }
-        __syncthreads();
-        // ---- phase 1: logits of every entity pair and head (as rsa_pool_kernel)
+        RSA_BAR(0);
+        // ---- phase 1: logits of every entity pair and head, 16 x 16 tiles over the waves
         {
             constexpr int TI = (R + 15) / 16;
             constexpr int KS = DH / 4;
-            const int rl = lane & 15;
-            for (int t = w; t < NH * TI * TI; t += NT / 64) {
+            for (int t = w; t < ((RSA_ABLATE & 1) ? 0 : NH * TI * TI); t += NTB / 64) {
                 const int h = t / (TI * TI), ti = (t / TI) % TI, tj = t % TI;
-                const float* qp = &Qs[min(16 * ti + rl, R - 1) * LDSW + h * DH + KS * kq];
-                const float* kp = &Ks[min(16 * tj + rl, R - 1) * LDSW + h * DH + KS * kq];
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const float* qp = &Qs[min(16 * ti + cl, R - 1) * LDSW + h * DH + KS * kq];
+                const float* kp = &Ks[min(16 * tj + cl, R - 1) * LDSW + h * DH + KS * kq];
+                f32x4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int m = 0; m < KS; m += 4) {
-                    const float4 a = *reinterpret_cast<const float4*>(qp + m);
-                    const float4 bk = *reinterpret_cast<const float4*>(kp + m);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bk.x, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bk.y, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bk.z, acc, 0, 0, 0);
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bk.w, acc, 0, 0, 0);
+                    const float4 qa = *reinterpret_cast<const float4*>(qp + m);
+                    const float4 kb = *reinterpret_cast<const float4*>(kp + m);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(qa.x, kb.x, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(qa.y, kb.y, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(qa.z, kb.z, a, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x4f32(qa.w, kb.w, a, 0, 0, 0);
                 }
-                const int kr = 16 * tj + rl;
+                const int kr = 16 * tj + cl;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int qr = 16 * ti + 4 * kq + i;
-                    if (qr < R && kr < R) S[h * SH + qr * SW + kr] = acc[i] / sqrt_d;
+                    if (qr < R && kr < R) S[h * SHB + qr * SWB + kr] = a[i] / sqrt_d;
                 }
             }
         }
-        __syncthreads();
-        // ---- heads: project V_h through W_o,h, softmax of every set row, accumulate
-        f32x4 acc[TILES];
-#pragma unroll
-        for (int t = 0; t < TILES; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // softmax of set row t = (s, r) of head h over the set's members, scattered by
-        // entity: P[t][j] = weight of action row N + j (0 for j = s), P0[t] = state row s
-        auto softmax = [&](int h) {
-            if (tid < ROWS && !(RSA_ABLATE & 2)) {
-                // set s = the row's set, query = its member r; the keys of set s are the state
-                // row s (member 0) and the action rows N + j, j != s (members 1.., in j order):
-                // one scalar and five float4 reads of the query's logit row
-                const int s_ = (tid + z) / N, r = tid + z - s_ * N;
-                const float* srow = &S[h * SH + member(SWARM_RSA_BASELINES, N, s_, r) * SW];
+        RSA_BAR(1);
+        // softmax waves: every head's probabilities of group g's set rows into P buffer buf,
+        // scattered by entity (weight of action row N + j, 0 at j = s; P0 = the set's state row)
+        auto softmax = [&](int g, int buf) {
+            const int q = tid - MW * 64 + z;
+            if (q < NH * GR && !(RSA_ABLATE & 2)) {
+                const int h = q / GR, lrow = q - h * GR;
+                const int s_ = SETS * g + lrow / N, r = lrow % N;
+                // the keys of set s: state row s (member 0) and the action rows N + j, j != s
+                const float* srow = &S[h * SHB + member(SWARM_RSA_BASELINES, N, s_, r) * SWB];
                 float la[N];
 #pragma unroll
                 for (int c = 0; c < N / 4; ++c) {
@@ -484,178 +512,198 @@ __global__ void __launch_bounds__(NT) rsa_baselines_kernel(int B, const float* _
                     sum += la[jj];
                 }
                 const float inv = 1.0f / sum;
-#if RSA_P_WIDE
-                float* prow = &P[tid * PS];
+                float* ph = Pb + buf * PB + h * PH;
+                const int t = lrow >> 4, c = lrow & 15;
+                float4* p4 = reinterpret_cast<float4*>(ph) + t * 64 + c;
+                float* p1 = ph + GT * 64 * 4 + t * 64 + c;
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4) {
-                    *reinterpret_cast<float4*>(prow + PG * g4) =
-                        make_float4(la[5 * g4] * inv, la[5 * g4 + 1] * inv, la[5 * g4 + 2] * inv, la[5 * g4 + 3] * inv);
-                    prow[PG * g4 + 4] = la[5 * g4 + 4] * inv;
+                    p4[16 * g4] = make_float4(la[5 * g4] * inv, la[5 * g4 + 1] * inv, la[5 * g4 + 2] * inv,
+                                              la[5 * g4 + 3] * inv);
+                    p1[16 * g4] = la[5 * g4 + 4] * inv;
                 }
-#else
-                float4* prow = reinterpret_cast<float4*>(&P[tid * PS]);
-#pragma unroll
-                for (int c = 0; c < N / 4; ++c)
-                    prow[c] = make_float4(la[4 * c] * inv, la[4 * c + 1] * inv, la[4 * c + 2] * inv, la[4 * c + 3] * inv);
-#endif
-                P0[tid] = es * inv;
+                ph[GT * 64 * 5 + lrow] = es * inv;
             }
         };
-#pragma unroll 1
-        for (int h = 0; h < NH; ++h) {
-            // W_o fragments of this head for this wave's 16 columns: k-step ks of lane group
-            // kq is input feature h*DH + (DH/4) kq + ks (contiguous float4 A reads of V)
-            float wb[DH / 4];
-#pragma unroll
-            for (int ks = 0; ks < DH / 4; ++ks) wb[ks] = Wo[col * HD + h * DH + (DH / 4) * kq + ks];
-            // VW_h[row][col] for the 2N rows (3 row tiles, rows >= 2N dropped)
-            constexpr int RT = (RSA_ABLATE & 8) ? 0 : (R + 15) / 16;
-#if RSA_VW_OVERLAP
-            // the three row tiles' MFMA chains first (their A operands read from LDS up front),
-            // then this head's softmax on the VALU while the matrix cores work, then the stores
-            f32x4 vacc[RT > 0 ? RT : 1];
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) vacc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int m = 0; m < DH / 4; m += 4) {
-#pragma unroll
-                for (int rt = 0; rt < RT; ++rt) {
-                    const float4 v = *reinterpret_cast<const float4*>(
-                        &Vs[min(16 * rt + cl, R - 1) * LDSW + h * DH + (DH / 4) * kq + m]);
-                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, wb[m + 0], vacc[rt], 0, 0, 0);
-                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, wb[m + 1], vacc[rt], 0, 0, 0);
-                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, wb[m + 2], vacc[rt], 0, 0, 0);
-                    vacc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, wb[m + 3], vacc[rt], 0, 0, 0);
-                }
-            }
-            softmax(h);
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = 16 * rt + 4 * kq + i;
-                    if (r < R) VW[r * LDSW + col] = vacc[rt][i];
-                }
-            }
-#else
-#pragma unroll
-            for (int rt = 0; rt < RT; ++rt) {
-                const float* vp = &Vs[min(16 * rt + cl, R - 1) * LDSW + h * DH + (DH / 4) * kq];
-                f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int m = 0; m < DH / 4; m += 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(vp + m);
-                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, wb[m + 0], a4, 0, 0, 0);
-                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, wb[m + 1], a4, 0, 0, 0);
-                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, wb[m + 2], a4, 0, 0, 0);
-                    a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, wb[m + 3], a4, 0, 0, 0);
-                    if (m % 16 == 12) __builtin_amdgcn_sched_barrier(0);
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int r = 16 * rt + 4 * kq + i;
-                    if (r < R) VW[r * LDSW + col] = a4[i];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            softmax(h);
-#endif
-            __syncthreads();
-            // acc[t] += P[rows of tile t][action j] VW_h[N + j][col]; k-step m of lane group kq
-            // is action j = (N/4) kq + m
-            if (!(RSA_ABLATE & 4)) {
-                float bv[N / 4];
-#pragma unroll
-                for (int m = 0; m < N / 4; ++m) bv[m] = VW[(N + (N / 4) * kq + m) * LDSW + col];
-#pragma unroll
-                for (int t = 0; t < TILES; ++t) {
-                    const float* ap = &P[(16 * t + cl) * PS + PG * kq];
-#if RSA_P_WIDE
-                    const float4 a4 = *reinterpret_cast<const float4*>(ap);
-                    const float a5 = ap[4];
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[0], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[1], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[2], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, bv[3], acc[t], 0, 0, 0);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a5, bv[4], acc[t], 0, 0, 0);
-#else
-#pragma unroll
-                    for (int m = 0; m < N / 4; ++m)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m], bv[m], acc[t], 0, 0, 0);
-#endif
-                    // keep the scheduler from hoisting every tile's A reads (register blow-up)
-                    if (RSA_GEMM_SCHED_BARRIER && t % 5 == 4) __builtin_amdgcn_sched_barrier(0);
-                }
-                // the state row of each set: rows 16t + 4kq + i (i < 4) belong to one set s
-#pragma unroll
-                for (int t = 0; t < TILES; ++t) {
-                    const int row0 = 16 * t + 4 * kq + z;
-                    const int s_ = row0 / N;
-                    const float4 p0 = *reinterpret_cast<const float4*>(&P0[row0]);
-                    const float vws = VW[s_ * LDSW + col];
-                    acc[t][0] += p0.x * vws;
-                    acc[t][1] += p0.y * vws;
-                    acc[t][2] += p0.z * vws;
-                    acc[t][3] += p0.w * vws;
-                    if (t % 5 == 4) __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            __syncthreads();
-        }
-        // ---- epilogue per group of 4 sets: bias + residual, LayerNorm, mean over the set
-#pragma unroll
-        for (int g = 0; g < GROUPS; ++g) {
-#pragma unroll
-            for (int tt = 0; tt < SETS * N / 16; ++tt) {
-                const int t = g * (SETS * N / 16) + tt;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = 16 * t + 4 * kq + i + z;      // set row of the env
-                    const int s_ = row / N, r = row - s_ * N;
-                    const float xr = Xs[member(SWARM_RSA_BASELINES, N, s_, r) * LDSW + col];
-                    PF[(row - g * SETS * N) * LDSW + col] = (acc[t][i] + bias) + xr;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            __syncthreads();
-            const int wave = w & (SETS - 1), half = w >> 2;
-            // row statistics: 4 lanes per row (32 columns each), quad reductions (DPP)
-            if (tid < 4 * SETS * N && !(RSA_ABLATE & 16)) {
-                const int row = tid >> 2, part = tid & 3;
-                const float4* fr = reinterpret_cast<const float4*>(&PF[row * LDSW + 32 * part]);
-                float4 v[8];
-#pragma unroll
-                for (int c = 0; c < 8; ++c) v[c] = fr[c];
-                float sum = 0.0f;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) sum += (v[c].x + v[c].y) + (v[c].z + v[c].w);
-                sum += __shfl_xor(sum, 1, 4);
-                sum += __shfl_xor(sum, 2, 4);
-                const float mean = sum * (1.0f / HD);
-                float sq = 0.0f;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const float d0 = v[c].x - mean, d1 = v[c].y - mean, d2 = v[c].z - mean, d3 = v[c].w - mean;
-                    sq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
-                }
-                sq += __shfl_xor(sq, 1, 4);
-                sq += __shfl_xor(sq, 2, 4);
-                if (part == 0) {
-                    stats[2 * row] = mean;
-                    stats[2 * row + 1] = 1.0f / sqrtf(sq * (1.0f / HD) + 1e-5f);
-                }
-            }
-            __syncthreads();
-            if (!(RSA_ABLATE & 16)) {
-                const int pc = 64 * half + lane;
-                const float* st = &stats[wave * 2 * N];   // rows wave * N + r of the group
-                float p0 = 0.0f;
+        // product waves (512 lanes = 4 sets x 128 columns): LayerNorm and the mean over each set of
+        // group g, from the group's rows and row statistics in LDS
+        auto set_means = [&](int g, int zg) {
+            if (RSA_ABLATE & 16) return;
+            const int set = (tid + zg) / HD, pc = (tid + zg) % HD;
+            const float* st = &stats[set * 2 * N];   // rows set * N + r of the group
+            float p0 = 0.0f;
 #pragma unroll 4
-                for (int r = 0; r < N; ++r) p0 += (PF[(wave * N + r) * LDSW + pc] - st[2 * r]) * st[2 * r + 1];
-                pooled[((size_t)e * N + g * SETS + wave) * HD + pc] = p0 / (float)N;
+            for (int r = 0; r < N; ++r) p0 += (PF[(set * N + r) * LDSW + pc] - st[2 * r]) * st[2 * r + 1];
+            pooled[((size_t)e * N + g * SETS + set) * HD + pc] = p0 / (float)N;
+        };
+        // The two roles run separate code paths (so neither carries the other's registers) with
+        // the same sequence of barriers: one after the prologue, three per group of 4 sets.
+        // Per group g:
+        //   product waves: the set means of group g - 1 (its rows and statistics are in LDS), then
+        //     group g's rows into registers;   softmax waves: group g + 1's probabilities;
+        //   barrier B1; product waves store group g's rows; barrier B2;
+        //   softmax waves: residual + row statistics of group g, then the residual loads of group
+        //     g + 1 (in flight across the barriers, which wait on LDS only); barrier B3.
+        if (prod) {
+            // lane ids made opaque per env (z): their address arithmetic is not hoisted out of
+            // the env loop into registers held across it
+            const int clz = cl + z, kqz = kq + z, colz = col + z;
+            // ---- this wave's 16 columns of VW_h = V_h W_o,h^T for every head: state rows into
+            // the slab, the action rows' B fragments (rows N + 5 kq + m) into bv
+            float bv[NH][N / 4];
+            // W_o's B fragments of every head for this wave's columns, all loads in flight at
+            // once (k-step ks of lane group kq of head h is input feature h*DH + (DH/4) kq + ks)
+            float wbh[HD / 4];
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+#pragma unroll
+                for (int ks = 0; ks < DH / 4; ++ks)
+                    wbh[h * (DH / 4) + ks] = Wo[colz * HD + h * DH + (DH / 4) * kqz + ks];
+#pragma unroll
+            for (int h = 0; h < NH; ++h) {
+                const float* wb = &wbh[h * (DH / 4)];
+#pragma unroll
+                for (int rt = 0; rt < ((RSA_ABLATE & 8) ? 0 : (R + 15) / 16); ++rt) {
+                    const float* vp = &Vs[min(16 * rt + clz, R - 1) * LDSW + h * DH + (DH / 4) * kqz];
+                    f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int m = 0; m < DH / 4; m += 4) {
+                        const float4 v = *reinterpret_cast<const float4*>(vp + m);
+                        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.x, wb[m + 0], a4, 0, 0, 0);
+                        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.y, wb[m + 1], a4, 0, 0, 0);
+                        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.z, wb[m + 2], a4, 0, 0, 0);
+                        a4 = __builtin_amdgcn_mfma_f32_16x16x4f32(v.w, wb[m + 3], a4, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int r = 16 * rt + 4 * kqz + i;
+                        if (r < N)
+                            VWS[((w * NH + h) * N + r) * 16 + clz] = a4[i];
+                        else if (r < R)
+                            Us[(w * N + r - N) * 16 + clz] = a4[i];
+                    }
+                }
+                // the wave's own hand-over tile: its LDS accesses complete in issue order
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+                for (int m = 0; m < N / 4; ++m) bv[h][m] = Us[(w * N + (N / 4) * kqz + m) * 16 + clz];
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            __syncthreads();
+            RSA_BAR(2);
+#pragma unroll 1
+            for (int g = 0; g < GROUPS; ++g) {
+                // opaque per group: the lane-derived LDS addresses below are recomputed per group
+                int zg;
+                asm volatile("s_mov_b32 %0, 0" : "=s"(zg));
+                const int lg = lane + zg, kqg = kq + zg;
+                if (g > 0) set_means(g - 1, zg);
+                const float* pb = Pb + (g & 1) * PB;
+                f32x4 a[GT];
+#pragma unroll
+                for (int tt = 0; tt < GT; ++tt) {
+                    a[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (!(RSA_ABLATE & 4)) {
+#pragma unroll
+                        for (int h = 0; h < NH; ++h) {
+                            const float* ph = pb + h * PH;
+                            const float4 a4 = reinterpret_cast<const float4*>(ph)[tt * 64 + lg];
+                            const float a5 = ph[GT * 64 * 4 + tt * 64 + lg];
+                            a[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[h][0], a[tt], 0, 0, 0);
+                            a[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[h][1], a[tt], 0, 0, 0);
+                            a[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[h][2], a[tt], 0, 0, 0);
+                            a[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, bv[h][3], a[tt], 0, 0, 0);
+                            a[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a5, bv[h][4], a[tt], 0, 0, 0);
+                        }
+                    }
+                    // rows 16tt + 4kq + i (i < 4) belong to one set: its state row, every head
+                    const int lrow0 = 16 * tt + 4 * kqg;
+                    const int s_ = SETS * g + lrow0 / N;
+#pragma unroll
+                    for (int h = 0; h < NH; ++h) {
+                        const float4 q = *reinterpret_cast<const float4*>(&pb[h * PH + GT * 64 * 5 + lrow0]);
+                        const float vs = VWS[((w * NH + h) * N + s_) * 16 + cl + zg];
+                        a[tt][0] += q.x * vs;
+                        a[tt][1] += q.y * vs;
+                        a[tt][2] += q.z * vs;
+                        a[tt][3] += q.w * vs;
+                    }
+                    // two tiles' fragments in flight at a time (register budget of 4 waves per SIMD)
+                    if (tt % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+                }
+                RSA_BAR(3 + 3 * g);   // B1: the set means of group g - 1 are done with the rows' LDS
+#pragma unroll
+                for (int tt = 0; tt < GT; ++tt)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) PF[(16 * tt + 4 * kqg + i) * LDSW + col] = a[tt][i] + bias;
+                RSA_BAR(4 + 3 * g);   // B2: the group's rows are stored
+                RSA_BAR(5 + 3 * g);   // B3: their statistics are stored
+            }
+            set_means(GROUPS - 1, z);
+        } else {
+            float4 xres[8];
+            // this lane's quarter of a set row's residual (its entity row of x) for group g,
+            // float4s 4c + part (a quad's loads cover 64 contiguous bytes per instruction)
+            const int q = tid - MW * 64;
+            const bool stat_lane = q < 4 * GR;
+            auto load_res = [&](int g) {
+                const int row = (q >> 2) + z, part = q & 3;
+                const int s_ = SETS * g + row / N, r = row % N;
+                const float4* xp = reinterpret_cast<const float4*>(xe + member(SWARM_RSA_BASELINES, N, s_, r) * HD);
+#pragma unroll
+                for (int c = 0; c < 8; ++c) xres[c] = (RSA_ABLATE & 32) ? float4{} : xp[4 * c + part];
+            };
+            if (stat_lane) load_res(0);
+            softmax(0, 0);
+            RSA_BAR(2);
+#pragma unroll 1
+            for (int g = 0; g < GROUPS; ++g) {
+                int zg;
+                asm volatile("s_mov_b32 %0, 0" : "=s"(zg));
+                if (g + 1 < GROUPS) softmax(g + 1, (g + 1) & 1);
+                RSA_BAR(3 + 3 * g);   // B1
+                RSA_BAR(4 + 3 * g);   // B2
+                // row statistics: bias + fc_out rows plus the residual, written back; 4 lanes per
+                // row (32 columns each), quad reductions (DPP)
+                if (stat_lane && !(RSA_ABLATE & 16)) {
+                    const int row = (q + zg) >> 2, part = q & 3;
+                    float4* fr = reinterpret_cast<float4*>(&PF[row * LDSW]) + part;   // float4s 4c + part
+                    float4 v[8];
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        v[c] = fr[4 * c];
+                        v[c].x += xres[c].x;
+                        v[c].y += xres[c].y;
+                        v[c].z += xres[c].z;
+                        v[c].w += xres[c].w;
+                        fr[4 * c] = v[c];
+                    }
+                    float sum = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) sum += (v[c].x + v[c].y) + (v[c].z + v[c].w);
+                    sum += __shfl_xor(sum, 1, 4);
+                    sum += __shfl_xor(sum, 2, 4);
+                    const float mean = sum * (1.0f / HD);
+                    float sq = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        const float d0 = v[c].x - mean, d1 = v[c].y - mean, d2 = v[c].z - mean, d3 = v[c].w - mean;
+                        sq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+                    }
+                    sq += __shfl_xor(sq, 1, 4);
+                    sq += __shfl_xor(sq, 2, 4);
+                    if (part == 0) {
+                        stats[2 * row] = mean;
+                        stats[2 * row + 1] = 1.0f / sqrtf(sq * (1.0f / HD) + 1e-5f);
+                    }
+                }
+                if (g == 2) RSA_STAMP(38);
+                if (stat_lane && g + 1 < GROUPS) load_res(g + 1);
+                if (g == 2) RSA_STAMP(39);
+                RSA_BAR(5 + 3 * g);   // B3
+            }
         }
+        RSA_BAR(3 + 3 * GROUPS);   // the next env's staging reuses the rows' LDS
     }
 }
 
@@ -727,7 +775,7 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
     const bool n20 = N == NMAX;  // the reference swarm: compile-time set size
     const bool shared_vw = RSA_SHARED_VW && n20 && mode == SWARM_RSA_BASELINES;
 #define RSA_LAUNCH(NH)                                                                                   \
-    (shared_vw ? rsa_baselines_kernel<NH><<<grid, NT, 0, s>>>(B, x, qkv, w_out, b_out, pooled)            \
+    (shared_vw ? rsa_baselines_kernel<NH><<<grid, NTB, 0, s>>>(B, x, qkv, w_out, b_out, pooled)            \
      : n20     ? rsa_pool_kernel<NH, NMAX><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled)   \
                : rsa_pool_kernel<NH, 0><<<grid, NT, 0, s>>>(mode, B, N, x, qkv, w_out, b_out, pooled))
     if (heads == 1)
@@ -739,6 +787,13 @@ int32_t swarm_rsa_pool(int32_t mode, int32_t B, int32_t N, int32_t heads, int32_
 #undef RSA_LAUNCH
     return swarm::record_hip_status();
 }
+
+#if RSA_TRACE
+int32_t swarm_debug_critic_trace(unsigned long long* out, size_t n) {
+    if (n != sizeof(g_rsa_trace) / sizeof(g_rsa_trace[0])) return SWARM_ERR_ARG;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rsa_trace), sizeof(g_rsa_trace)) == hipSuccess ? SWARM_OK : SWARM_ERR_ARG;
+}
+#endif
 
 int32_t swarm_rsa_pool_focal(int32_t B, int32_t N, int32_t A, int32_t heads, int32_t hidden, const float* x,
                              const float* qkv, const float* w_out, const float* b_out, const int64_t* focal,

@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--heads", type=int, default=4)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--cpu-envs", type=int, default=64)
+    ap.add_argument("--kernel-only", action="store_true", help="time the rsa_pool kernel alone")
     args = ap.parse_args()
     E, N, h, H = args.envs, 20, 128, args.heads
     dev = torch.device("cuda:0")
@@ -105,6 +106,8 @@ def main():
                               "executes executed_mfma_flops (fc_out folded into the values)",
                       "config": cfg}), flush=True)
 
+    if args.kernel_only:
+        return
     # ---- what the rollout calls per decision (no_grad), fused vs PyTorch path
     def rollout_calls():
         with torch.no_grad():

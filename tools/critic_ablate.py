@@ -20,7 +20,7 @@ out = torch.empty(E * N, h, device=dev)
 p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 res = {}
 first = None
-for path in sorted(glob.glob(os.path.join(ROOT, "build/ablate/libcritic_*.so"))):
+for path in sorted(glob.glob(os.path.join(ROOT, os.environ.get("ABL_DIR", "build/variants/critic_ablate"), "libcritic_*.so"))):
     lib = C.CDLL(path)
     lib.swarm_rsa_pool.argtypes = [C.c_int32] * 5 + [C.c_void_p] * 6
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)

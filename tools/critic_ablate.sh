@@ -1,9 +1,9 @@
 #!/bin/bash
 # Build timing-only ablation variants of the critic kernel as standalone .so files
-# (build/ablate/libcritic_<mask>.so); time them with tools/critic_ablate.py on the GPU.
+# (build/variants/critic_ablate/libcritic_<mask>.so; ABL_DIR overrides); time them with tools/critic_ablate.py on the GPU.
 set -e
 cd "$(dirname "$0")/../swarmacb-isaaclab_amd/csrc"
-OUT=../../build/ablate
+OUT=../../${ABL_DIR:-build/variants/critic_ablate}
 mkdir -p $OUT
 cat > $OUT/stub.cpp <<'EOS'
 #include <hip/hip_runtime.h>
