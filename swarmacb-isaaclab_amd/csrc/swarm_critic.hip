@@ -185,11 +185,26 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
             }
         }
         __syncthreads();
+        float touch0 = 0.0f, touch1 = 0.0f;
         // ---- phase 2: sets in chunks of SETS (waves w and w + 4 own set s0 + w)
         for (int s0 = 0; s0 < n_sets; s0 += SETS) {
             const int set = s0 + wave;
             const bool have = set < n_sets;
             float* P = &PF[wave * NH * PHS];
+            if (s0 + SETS >= n_sets && it + (int)gridDim.x < iters) {
+                // last chunk: touch every 128-byte line of the next iteration's x and q | k | v
+                // rows, so its staging (phase 0) reads L2 instead of HBM (as rsa_baselines_kernel)
+                const int en = single ? (it + (int)gridDim.x) * SINGLE_ENVS : it + (int)gridDim.x;
+                const int rows_n = (single ? min(SINGLE_ENVS, B - en) : 1) * erows;
+                const int lx = rows_n * HD / 32, lq = rows_n * 3 * HD / 32;
+                auto line = [&](int l) {
+                    return l < lx ? X[(size_t)en * erows * HD + (size_t)l * 32]
+                                  : QKV[(size_t)en * erows * 3 * HD + (size_t)(l - lx) * 32];
+                };
+                // up to two lines per thread, each load's value consumed only after the chunk
+                if (tid < lx + lq) touch0 = line(tid);
+                if (tid + NT < lx + lq) touch1 = line(tid + NT);
+            }
             // 2a-1: softmax over the set's members for every (row, head)
             if (have && !(RSA_ABLATE & 2)) {
                 for (int p = lane + 64 * half; p < N * NH; p += 128) {
@@ -322,6 +337,7 @@ __global__ void __launch_bounds__(NT) rsa_pool_kernel(int mode, int B, int n_rt,
             }
             __syncthreads();
         }
+        asm volatile("" ::"v"(touch0), "v"(touch1));   // the touch loads complete within the iteration
     }
 }
 
@@ -656,11 +672,20 @@ __global__ void __launch_bounds__(NTB) rsa_baselines_kernel(int B, const float* 
             if (stat_lane) load_res(0);
             softmax(0, 0);
             RSA_BAR(2);
+            float touch = 0.0f;
 #pragma unroll 1
             for (int g = 0; g < GROUPS; ++g) {
                 int zg;
                 asm volatile("s_mov_b32 %0, 0" : "=s"(zg));
-                if (g + 1 < GROUPS) softmax(g + 1, (g + 1) & 1);
+                if (g + 1 < GROUPS) {
+                    softmax(g + 1, (g + 1) & 1);
+                } else if (e + (int)gridDim.x < B && q < R * 3 * HD / 32) {
+                    // the last group has no next probabilities: touch every 128-byte line of the
+                    // next env's q | k | v rows instead, so its staging (phase 0) reads L2, not HBM
+                    // (1.415 -> 1.285 ms per C3 launch; touching its entity rows too: 1.37 ms,
+                    // profiles/r05/train/critic_prefetch_ab.txt)
+                    touch = QKV[((size_t)(e + gridDim.x) * R * 3 * HD) + (size_t)q * 32];
+                }
                 RSA_BAR(3 + 3 * g);   // B1
                 RSA_BAR(4 + 3 * g);   // B2
                 // row statistics: bias + fc_out rows plus the residual, written back; 4 lanes per
@@ -702,6 +727,7 @@ __global__ void __launch_bounds__(NTB) rsa_baselines_kernel(int B, const float* 
                 if (g == 2) RSA_STAMP(39);
                 RSA_BAR(5 + 3 * g);   // B3
             }
+            asm volatile("" ::"v"(touch));   // the touch loads complete before the env ends
         }
         RSA_BAR(3 + 3 * GROUPS);   // the next env's staging reuses the rows' LDS
     }

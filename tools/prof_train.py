@@ -61,12 +61,21 @@ def main():
     ks = prof.key_averages(group_by_input_shape=True)
     print(ks.table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=40,
                    max_shapes_column_width=110))
+    # every GEMM and reduction by input shape (device time per optimizer step)
+    for e in sorted(ks, key=lambda e: -e.self_device_time_total):
+        if e.key in ("aten::mm", "aten::addmm", "aten::bmm", "aten::sum", "aten::mul", "aten::cat", "aten::add",
+                     "aten::copy_") and e.self_device_time_total > 0:
+            print(f"SHAPE {e.self_device_time_total / a.steps:8.1f} us/step {e.count / a.steps:5.1f} calls/step "
+                  f"{e.key:12s} {e.input_shapes}")
     if a.stack:
         glue = ("aten::fill_", "aten::zero_", "aten::copy_", "aten::add", "aten::add_", "aten::cat",
-                "aten::index_put_", "aten::sum", "aten::mul", "aten::clone")
+                "aten::index_put_", "aten::sum", "aten::mul", "aten::clone", "aten::eq", "aten::ne", "aten::abs",
+                "aten::all", "aten::where", "aten::index", "aten::gather", "aten::sub", "aten::div", "aten::neg",
+                "aten::exp", "aten::log", "aten::mean", "aten::maximum", "aten::clamp", "aten::bmm", "aten::mm",
+                "aten::addmm", "aten::silu", "aten::silu_backward", "aten::_foreach_norm", "aten::stack")
         rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in glue and e.self_device_time_total > 0]
         rows.sort(key=lambda e: -e.self_device_time_total)
-        for e in rows[:40]:
+        for e in rows[:int(os.environ.get('PROF_ROWS', 40))]:
             print(f"{e.self_device_time_total / a.steps:9.1f} us/step  {e.count / a.steps:5.1f} calls/step  {e.key}")
             for fr in e.stack[:8]:
                 if "SwarmACB_isaac" in fr or "torch/autograd" in fr or "torch/nn" in fr:
