@@ -135,6 +135,30 @@ int32_t swarm_splitk_colsum(int64_t rows, int32_t out, int32_t slab, const float
 int32_t swarm_splitk_finish(int32_t chunks, int64_t n_w, const float* pw, float* dw, int32_t slabs, int32_t n_b,
                             const float* pb, float* db, void* stream);
 
+/* Weight and bias gradients of a linear layer y = x_1 W_1^T [+ x_2 W_2^T] [+ b] over `rows` rows in ONE
+ * launch (replaces the library GEMM dy^T x + the column sum torch's autograd issues per nn.Linear /
+ * nn.LSTM weight: reference agents/poca_networks.py:58-113 layers, trained by
+ * learned_option_critic_trainer.py:1421-1660 and poca_trainer.py:781-1050):
+ *   dw_k[o][j] = sum_r dy[r][o] x_k[r][j]   (k < n_src <= 2; dw_k: out x in_k, row-major, overwritten),
+ *   db[o] = sum_r dy[r][o]                 (db may be NULL),
+ * summed in a fixed order (deterministic). dy: rows x out, row stride ldy >= out. Source mode 0: x_k is
+ * rows x in_k with row stride ld. Mode 1 (an LSTM's previous hidden state, read in place): rows = n T,
+ * row n T + t of x_k is h0[n] (h0: n x in_k contiguous) at t = 0, else x[n T + t - 1] * keep[n T + t - 1]
+ * (x: the hidden sequence with row stride ld; keep: n T floats, or NULL = no mask). */
+typedef struct {
+    int32_t in;          /* columns of x_k (the layer's input features) */
+    int32_t mode;        /* 0 plain rows, 1 previous hidden state of a sequence */
+    int64_t ld;          /* row stride of x (floats) */
+    const float* x;
+    float* dw;
+    const float* h0;     /* mode 1 */
+    const float* keep;   /* mode 1, may be NULL */
+    int32_t T;           /* mode 1: steps per sequence */
+    int32_t pad;
+} swarm_wgrad_src_t;
+int32_t swarm_wgrad(int64_t rows, int32_t out, const float* dy, int64_t ldy, int32_t n_src,
+                    const swarm_wgrad_src_t* src, float* db, void* stream);
+
 /* The PPO trust-region loss terms of every trainer (ML-Agents trust_region_value_loss /
  * trust_region_policy_loss, reference agents/poca_trainer.py:144-191; the log-ratio-bounded policy loss
  * of learned_option_critic_trainer.py:45-72 with stable = 1) as masked means over M rows:

@@ -78,7 +78,8 @@ TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa
                  "swarm_ppo_policy_loss", "swarm_ppo_policy_loss_backward", "swarm_categorical_terms",
                  "swarm_categorical_terms_backward", "swarm_oc2_termination_terms",
                  "swarm_oc2_termination_terms_backward", "swarm_oc2_option_terms", "swarm_oc2_attention_terms",
-                 "swarm_oc2_attention_terms_backward", "swarm_oc2_action_terms", "swarm_oc2_action_terms_backward"]
+                 "swarm_oc2_attention_terms_backward", "swarm_oc2_action_terms", "swarm_oc2_action_terms_backward",
+                 "swarm_wgrad"]
 NORM_WIDTHS = (128, 256)   # row widths of swarm_row_norm_* / swarm_set_pool_*
 LSTM_MAX_BATCH = 6     # SWARM_LSTM_MAX_BATCH (include/swarmtrain.h)
 OC2_PARTIALS_FLOATS = 2048 * 24   # SWARM_OC2_PARTIALS_FLOATS (include/swarmtrain.h)
@@ -87,6 +88,12 @@ OC2_PARTIALS_FLOATS = 2048 * 24   # SWARM_OC2_PARTIALS_FLOATS (include/swarmtrai
 class LstmSeqFwd(C.Structure):
     _fields_ = [("n", C.c_int64)] + [(f, C.c_void_p) for f in ("xg", "w_hh", "h0", "c0", "keep", "h_out", "c_out",
                                                                   "act")]
+
+
+class WgradSrc(C.Structure):
+    """swarm_wgrad_src_t (include/swarmtrain.h)."""
+    _fields_ = [("in_f", C.c_int32), ("mode", C.c_int32), ("ld", C.c_int64), ("x", C.c_void_p), ("dw", C.c_void_p),
+                ("h0", C.c_void_p), ("keep", C.c_void_p), ("T", C.c_int32), ("pad", C.c_int32)]
 
 
 class LstmSeqBwd(C.Structure):
@@ -204,6 +211,8 @@ def load() -> C.CDLL:
     lib.swarm_splitk_colsum.argtypes = [i64, i32, i32, vp, vp, vp]
     lib.swarm_splitk_finish.restype = i32
     lib.swarm_splitk_finish.argtypes = [i32, i64, vp, vp, i32, i32, vp, vp, vp]
+    lib.swarm_wgrad.restype = i32
+    lib.swarm_wgrad.argtypes = [i64, i32, vp, i64, i32, vp, vp, vp]
     f32 = C.c_float
     lib.swarm_ppo_value_loss.restype = i32
     lib.swarm_ppo_value_loss.argtypes = [i64, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp]

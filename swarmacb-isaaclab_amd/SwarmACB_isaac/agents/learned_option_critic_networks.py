@@ -87,10 +87,7 @@ def _option_heads(head_lists, feats: torch.Tensor) -> list[torch.Tensor]:
     b = torch.stack([torch.cat([hl[o].bias for hl in head_lists], 0) for o in range(O)])       # (O, K)
     lead = feats.shape[:-2]
     x = feats.reshape(-1, H)
-    if x.is_cuda and torch.is_grad_enabled() and x.shape[0] >= _PN.SPLITK_MIN_ROWS:
-        y = _PN._SplitKLinear.apply(x.contiguous(), w, None)   # the weight gradient over row chunks
-    else:
-        y = torch.nn.functional.linear(x, w)
+    y = _PN._rows_linear(x, w, None)   # the weight gradient by row count (split rows / swarm_wgrad)
     y = y.view(-1, O, O, K)
     y = torch.diagonal(y, dim1=1, dim2=2).transpose(1, 2) + b                                # (rows, O, K)
     return [t.reshape(*lead, O, n) for t, n in zip(torch.split(y, outs, dim=-1), outs)]

@@ -37,7 +37,8 @@ _KERNEL_INITS = {
 }
 
 
-SPLITK_MIN_ROWS = 4096     # rows from which a layer's weight gradient is split over row chunks (A/B: profiles/r04/train/splitk_rows_ab.txt)
+# rows from which a layer's weight gradient is split over row chunks (A/B: profiles/r04/train/splitk_rows_ab.txt)
+SPLITK_MIN_ROWS = int(os.environ.get("SWARM_SPLITK_MIN_ROWS", "4096"))
 SPLITK_CHUNK_ROWS = 1024   # rows per chunk of that split
 SPLITK_SLAB_ROWS = 256     # rows per column-sum slab of its bias gradient
 # False (or SWARM_SPLITK_SUMS=0): the chunk / bias sums run torch's reductions
@@ -105,17 +106,91 @@ def _split_rows_weight_grad(dy, x, has_bias: bool):
     return dw, db
 
 
+# Layers over [WGRAD_MIN_ROWS, SPLITK_MIN_ROWS) rows (the update's 2,048-row minibatch MLPs and LSTM
+# inputs) take their weight and bias gradients from ONE swarm_wgrad launch instead of the library's
+# (out x in) GEMM with a 2,048-deep reduction (14-28 us each at C5) plus a column-sum kernel.
+WGRAD_MIN_ROWS = 128
+WGRAD_NATIVE = os.environ.get("SWARM_WGRAD", "1") != "0"
+
+
+def _wgrad_src(x: torch.Tensor, mode: int = 0, h0=None, keep=None, T: int = 0):
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    return x, _native.WgradSrc(x.shape[-1], mode, x.stride(-2), x.data_ptr(), None,
+                               h0.data_ptr() if h0 is not None else None,
+                               keep.data_ptr() if keep is not None else None, T, 0)
+
+
+def wgrad(dy: torch.Tensor, sources, with_bias: bool):
+    """([dy^T x_k for each source], column sums of dy or None) in one swarm_wgrad launch; sources
+    are _wgrad_src() pairs (tensor kept alive, descriptor)."""
+    if dy.stride(-1) != 1:
+        dy = dy.contiguous()
+    rows, out_f = dy.shape
+    dws, descs = [], []
+    for x, d in sources:
+        dw = torch.empty(out_f, d.in_f, dtype=dy.dtype, device=dy.device)
+        d.dw = dw.data_ptr()
+        dws.append(dw)
+        descs.append(d)
+    db = torch.empty(out_f, dtype=dy.dtype, device=dy.device) if with_bias else None
+    arr = (_native.WgradSrc * len(descs))(*descs)
+    lib = _native.load()
+    stream = C.c_void_p(torch.cuda.current_stream(dy.device).cuda_stream)
+    _native.check(lib.swarm_wgrad(rows, out_f, _ptr(dy), dy.stride(0), len(descs), C.cast(arr, C.c_void_p),
+                                  _ptr(db), stream), "swarm_wgrad")
+    return dws, db
+
+
+class _RowsWgradLinear(torch.autograd.Function):
+    """y = x W^T [+ x2 W2^T] [+ b] (addmm, as F.linear) whose weight and bias gradients come from
+    ONE swarm_wgrad launch (dx, dx2: library GEMMs). x2 / W2 carry a second product into the same
+    output, e.g. an LSTM step's [x | h0] [W_ih | W_hh]^T without concatenating either side."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, x2, weight2):
+        y = torch.addmm(bias, x, weight.t()) if bias is not None else x.mm(weight.t())
+        if x2 is not None:
+            y.addmm_(x2, weight2.t())
+        ctx.save_for_backward(x, weight, x2, weight2)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, x2, weight2 = ctx.saved_tensors
+        ng = ctx.needs_input_grad
+        dy = dy.contiguous()
+        dx = dy.mm(weight) if ng[0] else None
+        dx2 = dy.mm(weight2) if x2 is not None and ng[3] else None
+        srcs = [_wgrad_src(x)] + ([_wgrad_src(x2)] if x2 is not None else [])
+        dws, db = wgrad(dy, srcs, ctx.has_bias and ng[2])
+        return dx, dws[0] if ng[1] else None, db, dx2, (dws[1] if x2 is not None and ng[4] else None)
+
+
+def _rows_linear(x2d: torch.Tensor, weight, bias):
+    """F.linear over a 2-D input with the weight gradient routed by row count (GPU + autograd)."""
+    rows = x2d.shape[0]
+    if x2d.is_cuda and torch.is_grad_enabled() and x2d.dtype == torch.float32:
+        if rows >= SPLITK_MIN_ROWS:
+            return _SplitKLinear.apply(x2d.contiguous(), weight, bias)
+        if WGRAD_NATIVE and rows >= WGRAD_MIN_ROWS:
+            return _RowsWgradLinear.apply(x2d, weight, bias, None, None)
+    return torch.nn.functional.linear(x2d, weight, bias)
+
+
 class _Linear(nn.Linear):
-    """nn.Linear (same parameters and state-dict keys) whose GPU calls over at least
-    SPLITK_MIN_ROWS rows take the split-row weight gradient of _SplitKLinear."""
+    """nn.Linear (same parameters and state-dict keys) whose GPU calls with autograd take the
+    split-row weight gradient of _SplitKLinear (>= SPLITK_MIN_ROWS rows) or swarm_wgrad
+    (>= WGRAD_MIN_ROWS rows)."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not (x.is_cuda and torch.is_grad_enabled() and x.dtype == torch.float32):
             return super().forward(x)
         rows = x.numel() // x.shape[-1] if x.dim() else 0
-        if rows < SPLITK_MIN_ROWS:
+        if rows < WGRAD_MIN_ROWS or (rows < SPLITK_MIN_ROWS and not WGRAD_NATIVE):
             return super().forward(x)
-        y = _SplitKLinear.apply(x.reshape(rows, x.shape[-1]), self.weight, self.bias)
+        y = _rows_linear(x.reshape(rows, x.shape[-1]), self.weight, self.bias)
         return y.view(*x.shape[:-1], self.out_features)
 
 
@@ -238,13 +313,18 @@ class _LSTMSequences(torch.autograd.Function):
             dw = None
             if ctx.needs_input_grad[1 + 5 * i + 1]:
                 # W_hh's gradient: dgates^T h_prev' over every (sequence, step) row, one GEMM
-                prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
-                h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
                 rows = dxg.numel() // (4 * U)
-                if rows >= SPLITK_MIN_ROWS:   # a 12,288-deep reduction as one GEMM took 134 us
-                    dw = _split_rows_weight_grad(dxg.reshape(rows, 4 * U), h_prev.reshape(rows, U), False)[0]
+                if WGRAD_NATIVE and rows < SPLITK_MIN_ROWS:
+                    # h_prev read in place (h0 at t = 0, else the masked previous step)
+                    dw = wgrad(dxg.reshape(rows, 4 * U),
+                               [_wgrad_src(h_out.reshape(rows, U), 1, h0, keep, h_out.shape[1])], False)[0][0]
                 else:
-                    dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
+                    prev = h_out[:, :-1] if keep is None else h_out[:, :-1] * keep[:, :-1, None]
+                    h_prev = torch.cat([h0.unsqueeze(1), prev], dim=1)
+                    if rows >= SPLITK_MIN_ROWS:   # a 12,288-deep reduction as one GEMM took 134 us
+                        dw = _split_rows_weight_grad(dxg.reshape(rows, 4 * U), h_prev.reshape(rows, U), False)[0]
+                    else:
+                        dw = dxg.reshape(-1, 4 * U).t().mm(h_prev.reshape(-1, U))
             out += [dxg, dw, dh0, dc0, None]
         return tuple(out)
 
@@ -388,9 +468,9 @@ def lstm_sequences(items):
                 with torch.no_grad() if frozen else contextlib.nullcontext():
                     bias = lstm.bias_ih_l0 + lstm.bias_hh_l0
                     rows = seq.shape[0] * seq.shape[1]
-                    if torch.is_grad_enabled() and rows >= SPLITK_MIN_ROWS:
-                        xg = _SplitKLinear.apply(seq.reshape(rows, -1).contiguous(), lstm.weight_ih_l0,
-                                                 bias).view(seq.shape[0], seq.shape[1], -1)
+                    if torch.is_grad_enabled() and rows >= WGRAD_MIN_ROWS:
+                        xg = _rows_linear(seq.reshape(rows, -1), lstm.weight_ih_l0,
+                                          bias).view(seq.shape[0], seq.shape[1], -1)
                     else:
                         xg = torch.nn.functional.linear(seq, lstm.weight_ih_l0, bias)
                     w_hh = lstm.weight_hh_l0.contiguous()
@@ -426,6 +506,10 @@ def _lstm_single_step(lstm: nn.LSTM, seq: torch.Tensor, state):
         gates = _SplitKLinear.apply(torch.cat([x, h0], dim=1),
                                     torch.cat([lstm.weight_ih_l0, lstm.weight_hh_l0], dim=1),
                                     lstm.bias_ih_l0 + lstm.bias_hh_l0)
+    elif seq.is_cuda and torch.is_grad_enabled() and WGRAD_NATIVE and n >= WGRAD_MIN_ROWS:
+        # the same two products into one output; dW_ih, dW_hh and the bias gradient in one launch
+        gates = _RowsWgradLinear.apply(x, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0, h0,
+                                       lstm.weight_hh_l0)
     else:
         gates = torch.addmm(torch.nn.functional.linear(x, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0),
                             h0, lstm.weight_hh_l0.t())

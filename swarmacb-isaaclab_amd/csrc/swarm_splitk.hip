@@ -115,3 +115,123 @@ int32_t swarm_splitk_finish(int32_t chunks, int64_t n_w, const float* pw, float*
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// swarm_wgrad: the weight (and bias) gradients of y = x_1 W_1^T [+ x_2 W_2^T] [+ b] over R rows in
+// ONE launch (include/swarmtrain.h). torch forms each as its own library GEMM with an R-deep
+// reduction (dy^T x: an (out x in) output, i.e. a handful of output tiles, each a 2,048-deep
+// loop: 14-28 us at C5 for 67-134 MFLOP) plus a column-sum kernel for db. Here a workgroup owns
+// one 16 x 16 tile of one dW; its 8 waves split the rows, each accumulating its rows' products
+// on the matrix cores (v_mfma_f32_16x16x4f32: A = dy^T, B = x, 4 rows per instruction, exact
+// fp32 products) and, in the tiles of column block 0, the column sums of dy; the 8 partials
+// meet in LDS in wave order (deterministic). Source mode 1 reads the LSTM's previous hidden
+// state in place (row n T + t: h0[n] at t = 0, else h[n][t - 1] * keep[n][t - 1]), so dW_hh
+// needs no concatenated copy of the shifted sequence.
+namespace {
+
+typedef float f32x4_w __attribute__((ext_vector_type(4)));
+constexpr int kWgWaves = 8;
+constexpr int kWgUnroll = 4;
+
+struct WgradSrcs {
+    swarm_wgrad_src_t s[2];
+    int tiles0;   // column tiles of source 0 (source 1 follows)
+};
+
+__device__ __forceinline__ float wgrad_x(const swarm_wgrad_src_t& s, int64_t r, int i) {
+    if (s.mode == 0) return s.x[r * s.ld + i];
+    const int64_t n = r / s.T, t = r - n * s.T;
+    if (t == 0) return s.h0[n * s.in + i];
+    const float v = s.x[(r - 1) * s.ld + i];
+    return s.keep ? v * s.keep[r - 1] : v;
+}
+
+__global__ __launch_bounds__(64 * kWgWaves) void wgrad_kernel(int64_t R, int out, const float* __restrict__ dy,
+                                                               int64_t ldy, WgradSrcs S, float* __restrict__ db) {
+    __shared__ f32x4_w part[kWgWaves][64];
+    __shared__ float dpart[kWgWaves][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 15, kq = lane >> 4;
+    const int tile = blockIdx.x;
+    const int k = tile < S.tiles0 ? 0 : 1;
+    const swarm_wgrad_src_t& src = S.s[k];
+    const int i = 16 * (tile - (k ? S.tiles0 : 0)) + c;     // input column of this lane's B operand
+    const int o = 16 * blockIdx.y + c;                        // output column of this lane's A operand
+    const bool with_db = db != nullptr && tile == 0;
+    const bool oi = o < out, ii = i < src.in;
+    // the wave's rows: quads [q0, q1) of 4 rows, row 4 q + kq per lane
+    const int64_t quads = (R + 3) / 4;
+    const int64_t q0 = quads * w / kWgWaves, q1 = quads * (w + 1) / kWgWaves;
+    f32x4_w acc = {0.f, 0.f, 0.f, 0.f};
+    float ds = 0.0f;
+    int64_t q = q0;
+    for (; q + kWgUnroll <= q1; q += kWgUnroll) {
+        float a[kWgUnroll], b[kWgUnroll];
+#pragma unroll
+        for (int u = 0; u < kWgUnroll; ++u) {
+            const int64_t r = 4 * (q + u) + kq;
+            a[u] = (oi && r < R) ? dy[r * ldy + o] : 0.0f;
+            b[u] = (ii && r < R) ? wgrad_x(src, r, i) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kWgUnroll; ++u) {
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc, 0, 0, 0);
+            ds += a[u];
+        }
+    }
+    for (; q < q1; ++q) {
+        const int64_t r = 4 * q + kq;
+        const float a = (oi && r < R) ? dy[r * ldy + o] : 0.0f;
+        const float b = (ii && r < R) ? wgrad_x(src, r, i) : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        ds += a;
+    }
+    part[w][lane] = acc;
+    dpart[w][lane] = ds;
+    __syncthreads();
+    if (w != 0) return;
+    f32x4_w s = part[0][lane];
+#pragma unroll
+    for (int v = 1; v < kWgWaves; ++v) s += part[v][lane];
+    // D layout of the 16 x 16 tile: column lane & 15 (the input column i), rows 4 (lane >> 4) + v
+    const int icol = 16 * (tile - (k ? S.tiles0 : 0)) + c;
+    if (icol < src.in) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int orow = 16 * blockIdx.y + 4 * kq + v;
+            if (orow < out) src.dw[(int64_t)orow * src.in + icol] = s[v];
+        }
+    }
+    if (with_db && lane < 16) {
+        float t = 0.0f;
+        for (int v = 0; v < kWgWaves; ++v)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) t += dpart[v][16 * g + lane];
+        if (o < out) db[o] = t;
+    }
+}
+
+}  // namespace
+
+extern "C" int32_t swarm_wgrad(int64_t rows, int32_t out, const float* dy, int64_t ldy, int32_t n_src,
+                               const swarm_wgrad_src_t* src, float* db, void* stream) {
+    if (rows < 0 || out < 1 || n_src < 1 || n_src > 2 || !src || ldy < out) return SWARM_ERR_ARG;
+    WgradSrcs S{};
+    int tiles = 0;
+    for (int k = 0; k < n_src; ++k) {
+        const swarm_wgrad_src_t& s = src[k];
+        if (s.in < 1 || (rows > 0 && !s.x) || !s.dw || (s.mode != 0 && s.mode != 1)) return SWARM_ERR_ARG;
+        if (s.mode == 0 && s.ld < s.in) return SWARM_ERR_ARG;
+        if (s.mode == 1 && (s.T < 1 || (rows > 0 && !s.h0) || s.ld < s.in || rows % s.T)) return SWARM_ERR_ARG;
+        S.s[k] = s;
+        if (k == 0) S.tiles0 = (s.in + 15) / 16;
+        tiles += (s.in + 15) / 16;
+    }
+    if (n_src == 1) S.s[1] = S.s[0];
+    if (rows > 0 && !dy) return SWARM_ERR_ARG;
+    const int otiles = (out + 15) / 16;
+    if ((int64_t)tiles * otiles > 0x7fffffff || otiles > 65535) return SWARM_ERR_ARG;
+    wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)otiles), 64 * kWgWaves, 0, static_cast<hipStream_t>(stream)>>>(
+        rows, out, dy, ldy, S, db);
+    return hipGetLastError() == hipSuccess ? SWARM_OK : SWARM_ERR_HIP;
+}
