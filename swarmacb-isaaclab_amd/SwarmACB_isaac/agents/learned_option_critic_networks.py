@@ -75,16 +75,20 @@ class SquashedNormal:
         return self.base_dist.entropy()
 
 
-def _option_heads(head_lists, feats: torch.Tensor) -> list[torch.Tensor]:
+def _option_heads(head_lists, feats: torch.Tensor, stacked=None) -> list[torch.Tensor]:
     """[[head_o(feats[..., o, :]) for o] for every head kind] as ONE GEMM: every option's
     feature row meets the stacked weights of all options' heads (O x sum(out) columns,
     a few dozen), and the diagonal option blocks are kept. (..., O, H) -> per kind
-    (..., O, out)."""
+    (..., O, out). `stacked`: the actor's (W, b) storage its head Parameters alias
+    (LearnedOptionActor._stacked_heads); without it the weights are concatenated."""
     O, H = feats.shape[-2], feats.shape[-1]
     outs = [hl[0].out_features for hl in head_lists]
     K = sum(outs)
-    w = torch.cat([torch.cat([hl[o].weight for hl in head_lists], 0) for o in range(O)], 0)    # (O K, H)
-    b = torch.stack([torch.cat([hl[o].bias for hl in head_lists], 0) for o in range(O)])       # (O, K)
+    if stacked is not None:
+        w, b = stacked[0], stacked[1].view(O, K)                                                 # (O K, H), (O, K)
+    else:
+        w = torch.cat([torch.cat([hl[o].weight for hl in head_lists], 0) for o in range(O)], 0)
+        b = torch.stack([torch.cat([hl[o].bias for hl in head_lists], 0) for o in range(O)])
     lead = feats.shape[:-2]
     x = feats.reshape(-1, H)
     y = _PN._rows_linear(x, w, None)   # the weight gradient by row count (split rows / swarm_wgrad)
@@ -163,6 +167,31 @@ class LearnedOptionActor(nn.Module):
             self.log_std = nn.Parameter(torch.full((self.num_options, self.act_dim), float(initial_log_std)))
         # packed public memory: manager state + one state per option
         self.hidden_size = self.manager_hidden_size + self.num_options * self.option_recurrent_size
+        self._stack_heads()
+
+    # ---- the option heads' weights in one storage (no concatenation per forward)
+    def _head_kinds(self):
+        kinds = [self.option_value_heads, self.action_heads, self.termination_heads]
+        if self.separate_selector:
+            kinds.append(self.selector_heads)
+        return kinds
+
+    def _stack_heads(self):
+        """Every option head's weight and bias in one (O K, H) / (O K,) storage, option-major as
+        _option_heads multiplies them (poca_networks.StackedLinears: the head Parameters alias it)."""
+        kinds = self._head_kinds()
+        self.__dict__["_stacked"] = _PN.StackedLinears([hl[o] for o in range(self.num_options) for hl in kinds])
+
+    def _stacked_heads(self):
+        """(W, b) of the stacked heads with autograd through the head Parameters, or None (concatenate)."""
+        st = self.__dict__.get("_stacked")
+        return st.tensors() if st is not None else None
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        if "_stacked" in self.__dict__:
+            self._stacked.restack()
+        return out
 
     def option_log_stds(self) -> torch.Tensor:
         if not self.squash_actions:
@@ -264,7 +293,7 @@ class LearnedOptionActor(nn.Module):
         kinds = [self.option_value_heads, self.action_heads, self.termination_heads]
         if self.separate_selector:
             kinds.append(self.selector_heads)
-        heads = _option_heads(kinds, option_features)
+        heads = _option_heads(kinds, option_features, self._stacked_heads())
         option_values, action_means, termination_logits = heads[0].squeeze(-1), heads[1], heads[2].squeeze(-1)
         selector_logits = heads[3].squeeze(-1) if self.separate_selector else option_values
         action_stds = self.option_log_stds().exp().view(1, 1, O, self.act_dim).expand_as(action_means)

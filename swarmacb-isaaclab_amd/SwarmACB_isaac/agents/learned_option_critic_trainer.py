@@ -88,6 +88,15 @@ def stable_trust_region_policy_loss(advantages, log_probs, old_log_probs, epsilo
 FUSED_OC2_TERMS = os.environ.get("SWARM_FUSED_OC2_TERMS", "1") != "0"
 
 
+def _stack_f64(scalars) -> torch.Tensor:
+    """The detached scalars as one float64 vector: float32 ones are stacked first and converted
+    once (one kernel each way instead of one conversion per scalar; exact either way)."""
+    vals = [t.detach().reshape(()) for t in scalars]
+    if all(v.dtype == torch.float32 for v in vals):
+        return torch.stack(vals).double()
+    return torch.stack([v.double() for v in vals])
+
+
 def _vp(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -829,9 +838,8 @@ class LearnedOptionCriticTrainer(TrainerBase):
                                         self.critic_parameters, cfg.max_grad_norm)
         G["grad_norms"][1] += norm_c.double()
         G["bad"][3] |= ~torch.isfinite(norm_c)
-        G["totals"] += torch.stack([losses[n].detach().reshape(()).double() for n in METRIC_NAMES]
-                                   + [actor_loss.detach().double(), critic_loss.detach().double()]
-                                   + [terms[n].detach().reshape(()).double() for n in OBJECTIVE_NAMES[2:]])
+        G["totals"] += _stack_f64([losses[n] for n in METRIC_NAMES] + [actor_loss, critic_loss]
+                                  + [terms[n] for n in OBJECTIVE_NAMES[2:]])
         G["nb"] += 1.0
         return G["nb"]
 

@@ -194,6 +194,68 @@ class _Linear(nn.Linear):
         return y.view(*x.shape[:-1], self.out_features)
 
 
+class _StackedView(torch.autograd.Function):
+    """A stacked parameter storage as a differentiable function of the Parameters that alias it
+    (no copy): forward returns the storage itself, backward hands each Parameter its slice of
+    the gradient (what the backward of torch.cat over those Parameters would hand them)."""
+
+    @staticmethod
+    def forward(ctx, stacked, spans, *params):
+        ctx.spans = spans
+        return stacked.view_as(stacked)
+
+    @staticmethod
+    def backward(ctx, g):
+        flat = g.contiguous().reshape(-1)
+        return (None, None) + tuple(flat[a:b].view(shape) for a, b, shape in ctx.spans)
+
+
+class StackedLinears:
+    """The weights and biases of several Linear layers with one in_features, moved into one
+    (sum out, in) / (sum out,) storage in the given order; each layer's Parameter is re-pointed
+    (.data) to its slice, so the Parameter objects (optimizer state, state_dict keys, checkpoints)
+    are unchanged while a forward reads the stacked storage instead of concatenating the layers'
+    tensors per call (torch.cat: one kernel each for the weights and the biases)."""
+
+    def __init__(self, linears):
+        self.linears = list(linears)
+        self.restack()
+
+    def restack(self):
+        ref = self.linears[0].weight
+        H = ref.shape[1]
+        outs = [m.out_features for m in self.linears]
+        self.W = torch.empty(sum(outs), H, dtype=ref.dtype, device=ref.device)
+        self.B = torch.empty(sum(outs), dtype=ref.dtype, device=ref.device)
+        w_spans, b_spans, off = [], [], 0
+        with torch.no_grad():
+            for m, n in zip(self.linears, outs):
+                self.W[off:off + n].copy_(m.weight)
+                self.B[off:off + n].copy_(m.bias)
+                m.weight.data = self.W[off:off + n]
+                m.bias.data = self.B[off:off + n]
+                w_spans.append((off * H, (off + n) * H, (n, H)))
+                b_spans.append((off, off + n, (n,)))
+                off += n
+        self.w_spans, self.b_spans = tuple(w_spans), tuple(b_spans)
+
+    def intact(self) -> bool:
+        """Every Parameter still aliases the storage (a deepcopy or .to() gives them their own)."""
+        wp, bp, es = self.W.data_ptr(), self.B.data_ptr(), self.W.element_size()
+        return all(m.weight.data_ptr() == wp + a * es and m.bias.data_ptr() == bp + b0 * es
+                   for m, (a, _, _), (b0, _, _) in zip(self.linears, self.w_spans, self.b_spans))
+
+    def tensors(self):
+        """(W, B) as functions of the layers' Parameters, or None when the aliasing is broken
+        inside a graph capture (the caller concatenates); re-stacked here otherwise."""
+        if not self.intact():
+            if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+                return None
+            self.restack()
+        return (_StackedView.apply(self.W, self.w_spans, *[m.weight for m in self.linears]),
+                _StackedView.apply(self.B, self.b_spans, *[m.bias for m in self.linears]))
+
+
 def _linear_layer(input_size: int, output_size: int, kernel_init: str = "xavier_uniform",
                   kernel_gain: float = 1.0, bias_init: str = "zeros") -> nn.Linear:
     """ML-Agents-initialised linear layer (poca_networks.py:58-82)."""
@@ -729,6 +791,27 @@ class ResidualSelfAttention(nn.Module):
             setattr(self, name, _linear_layer(embed_dim, embed_dim, kernel_init="normal", kernel_gain=gain))
         self.embedding_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
         self.residual_norm = nn.LayerNorm(embed_dim, elementwise_affine=False)
+        # q | k | v in one storage (one projection GEMM without concatenating the weights)
+        self.__dict__["_qkv"] = StackedLinears([self.fc_q, self.fc_k, self.fc_v])
+
+    def qkv_params(self, grad: bool = True):
+        """(W_q | W_k | W_v, b_q | b_k | b_v): the stacked storage (with autograd through the layers'
+        Parameters when `grad`), or their concatenation when the storage cannot be used."""
+        if not grad:
+            if self._qkv.intact():
+                return self._qkv.W, self._qkv.B
+        else:
+            wb = self._qkv.tensors()
+            if wb is not None:
+                return wb
+        return (torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight]),
+                torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias]))
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        if "_qkv" in self.__dict__:
+            self._qkv.restack()
+        return out
 
     def _native_core(self, inp: torch.Tensor) -> bool:
         B, N, D = inp.shape
@@ -742,8 +825,7 @@ class ResidualSelfAttention(nn.Module):
             # both LayerNorms, the residual add and the set mean on swarm_row_norm_* /
             # swarm_set_pool_* (one pass each way instead of torch's layer_norm / add / mean)
             x2 = _RowNorm.apply(inp.reshape(B * N, D).contiguous())
-            w = torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight])
-            b = torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias])
+            w, b = self.qkv_params(torch.is_grad_enabled())
             if torch.is_grad_enabled() and B * N >= SPLITK_MIN_ROWS:
                 qkv = _SplitKLinear.apply(x2, w, b)
             else:
@@ -754,8 +836,7 @@ class ResidualSelfAttention(nn.Module):
         if self._native_core(inp):
             # the three projections as one GEMM (q | k | v column blocks), then the attention
             # core of every set and head in one MFMA kernel each way (_AttnCore)
-            w = torch.cat([self.fc_q.weight, self.fc_k.weight, self.fc_v.weight])
-            b = torch.cat([self.fc_q.bias, self.fc_k.bias, self.fc_v.bias])
+            w, b = self.qkv_params(torch.is_grad_enabled())
             x2 = x.reshape(B * N, D)
             if torch.is_grad_enabled() and B * N >= SPLITK_MIN_ROWS:
                 qkv = _SplitKLinear.apply(x2, w, b)
@@ -790,8 +871,7 @@ def _fused_rsa(attn: ResidualSelfAttention, rows: torch.Tensor, mode, n: int):
     _native.check(lib.swarm_rsa_embedding_norm(rows.numel() // attn.embed_dim, attn.embed_dim,
                                                C.c_void_p(rows.data_ptr()), C.c_void_p(x.data_ptr()), stream),
                   "swarm_rsa_embedding_norm")
-    w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
-    b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
+    w, b = attn.qkv_params(torch.is_grad_enabled())
     qkv = torch.nn.functional.linear(x, w, b).contiguous()
     wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
     out = []
@@ -973,8 +1053,7 @@ class POCACritic(nn.Module):
         _native.check(lib.swarm_rsa_embedding_norm(rows.numel() // attn.embed_dim, attn.embed_dim,
                                                    C.c_void_p(rows.data_ptr()), C.c_void_p(x.data_ptr()), stream),
                       "swarm_rsa_embedding_norm")
-        w = torch.cat([attn.fc_q.weight, attn.fc_k.weight, attn.fc_v.weight])
-        b = torch.cat([attn.fc_q.bias, attn.fc_k.bias, attn.fc_v.bias])
+        w, b = attn.qkv_params(torch.is_grad_enabled())
         qkv = torch.nn.functional.linear(x, w, b).contiguous()
         wo, bo = attn.fc_out.weight.contiguous(), attn.fc_out.bias.contiguous()
         focal = focal.contiguous()

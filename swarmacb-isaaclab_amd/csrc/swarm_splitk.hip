@@ -121,29 +121,79 @@ int32_t swarm_splitk_finish(int32_t chunks, int64_t n_w, const float* pw, float*
 // ONE launch (include/swarmtrain.h). torch forms each as its own library GEMM with an R-deep
 // reduction (dy^T x: an (out x in) output, i.e. a handful of output tiles, each a 2,048-deep
 // loop: 14-28 us at C5 for 67-134 MFLOP) plus a column-sum kernel for db. Here a workgroup owns
-// one 16 x 16 tile of one dW; its 8 waves split the rows, each accumulating its rows' products
+// one 16 x 16 tile of one dW; its 16 waves split the rows, each accumulating its rows' products
 // on the matrix cores (v_mfma_f32_16x16x4f32: A = dy^T, B = x, 4 rows per instruction, exact
-// fp32 products) and, in the tiles of column block 0, the column sums of dy; the 8 partials
+// fp32 products) and, in the tiles of column block 0, the column sums of dy; the 16 partials
 // meet in LDS in wave order (deterministic). Source mode 1 reads the LSTM's previous hidden
 // state in place (row n T + t: h0[n] at t = 0, else h[n][t - 1] * keep[n][t - 1]), so dW_hh
 // needs no concatenated copy of the shifted sequence.
 namespace {
 
 typedef float f32x4_w __attribute__((ext_vector_type(4)));
-constexpr int kWgWaves = 8;
-constexpr int kWgUnroll = 4;
+// 16 waves (4 per SIMD), each with up to 32 row quads' operands in flight (64 loads issued before
+// the first MFMA): the loop is bound by the latency of its operand loads (two 64-byte row pieces
+// per MFMA), not by the matrix cores; at 4 or 8 quads per batch every call took 12-17 us, the
+// batches' load latencies back to back (tools/bench_wgrad.py)
+constexpr int kWgWaves = 16;
+constexpr int kWgUnroll = 32;
 
 struct WgradSrcs {
     swarm_wgrad_src_t s[2];
     int tiles0;   // column tiles of source 0 (source 1 follows)
 };
 
-__device__ __forceinline__ float wgrad_x(const swarm_wgrad_src_t& s, int64_t r, int i) {
-    if (s.mode == 0) return s.x[r * s.ld + i];
-    const int64_t n = r / s.T, t = r - n * s.T;
-    if (t == 0) return s.h0[n * s.in + i];
-    const float v = s.x[(r - 1) * s.ld + i];
-    return s.keep ? v * s.keep[r - 1] : v;
+// The wave's rows [4 q0, 4 q1): operands loaded unconditionally from clamped addresses and zeroed
+// by selects (a branch per load put a wait on every load: the batch's loads must all be in flight
+// before the first MFMA); MODE / KEEP are template parameters so the loop carries no mode branch.
+template <int MODE, bool KEEP>
+__device__ __forceinline__ void wgrad_rows(int64_t R64, int out, const float* __restrict__ dy, int64_t ldy,
+                                           const swarm_wgrad_src_t& src, int o, int i, int kq, int64_t q0,
+                                           int64_t q1, f32x4_w& acc, float& ds) {
+    constexpr int U = MODE == 0 ? kWgUnroll : kWgUnroll / 2;   // mode 1 holds 3-4 loads per quad
+    // 32-bit element offsets (swarm_wgrad bounds rows x row stride < 2^31): one VALU op per address
+    // (64-bit offsets: 12.7 instead of 7.7 us per call; a separate unchecked path for whole
+    // batches: 9.6 us; tools/bench_wgrad.py under rocprofv3)
+    const uint32_t R = (uint32_t)R64, la = (uint32_t)ldy, lb = (uint32_t)src.ld;
+    const bool oi = o < out, ii = i < src.in;
+    const uint32_t oc = oi ? o : out - 1, ic = ii ? i : src.in - 1;
+    const float* __restrict__ X = src.x;
+    for (uint32_t q = (uint32_t)q0; q < (uint32_t)q1; q += U) {
+        float av[U], xv[U], hv[U], kv[U];
+        bool first[U];
+        // every load of the batch first (no consumer in between: one wait for the batch)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t r = 4 * (q + u) + kq;
+            const uint32_t rc = ((q + u < (uint32_t)q1) & (r < R)) ? r : 0u;
+            av[u] = dy[rc * la + oc];
+            if constexpr (MODE == 0) {
+                xv[u] = X[rc * lb + ic];
+            } else {
+                // row n T + t: h0[n] at t = 0, else h[n T + t - 1] (* keep[n T + t - 1])
+                const uint32_t n = rc / (uint32_t)src.T;
+                first[u] = rc == n * (uint32_t)src.T;
+                const uint32_t rp = rc > 0 ? rc - 1 : 0u;
+                hv[u] = src.h0[n * (uint32_t)src.in + ic];
+                xv[u] = X[rp * lb + ic];
+                if constexpr (KEEP) kv[u] = src.keep[rp];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t r = 4 * (q + u) + kq;
+            const bool ok = (q + u < (uint32_t)q1) & (r < R);
+            float bv = xv[u];
+            if constexpr (MODE == 1) {
+                if constexpr (KEEP) bv = bv * kv[u];
+                bv = first[u] ? hv[u] : bv;
+            }
+            const float a = (ok & oi) ? av[u] : 0.0f;
+            const float b = (ok & ii) ? bv : 0.0f;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+            ds += a;
+        }
+    }
 }
 
 __global__ __launch_bounds__(64 * kWgWaves) void wgrad_kernel(int64_t R, int out, const float* __restrict__ dy,
@@ -158,33 +208,18 @@ __global__ __launch_bounds__(64 * kWgWaves) void wgrad_kernel(int64_t R, int out
     const int i = 16 * (tile - (k ? S.tiles0 : 0)) + c;     // input column of this lane's B operand
     const int o = 16 * blockIdx.y + c;                        // output column of this lane's A operand
     const bool with_db = db != nullptr && tile == 0;
-    const bool oi = o < out, ii = i < src.in;
     // the wave's rows: quads [q0, q1) of 4 rows, row 4 q + kq per lane
     const int64_t quads = (R + 3) / 4;
     const int64_t q0 = quads * w / kWgWaves, q1 = quads * (w + 1) / kWgWaves;
     f32x4_w acc = {0.f, 0.f, 0.f, 0.f};
     float ds = 0.0f;
-    int64_t q = q0;
-    for (; q + kWgUnroll <= q1; q += kWgUnroll) {
-        float a[kWgUnroll], b[kWgUnroll];
-#pragma unroll
-        for (int u = 0; u < kWgUnroll; ++u) {
-            const int64_t r = 4 * (q + u) + kq;
-            a[u] = (oi && r < R) ? dy[r * ldy + o] : 0.0f;
-            b[u] = (ii && r < R) ? wgrad_x(src, r, i) : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < kWgUnroll; ++u) {
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc, 0, 0, 0);
-            ds += a[u];
-        }
-    }
-    for (; q < q1; ++q) {
-        const int64_t r = 4 * q + kq;
-        const float a = (oi && r < R) ? dy[r * ldy + o] : 0.0f;
-        const float b = (ii && r < R) ? wgrad_x(src, r, i) : 0.0f;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-        ds += a;
+    if (R > 0) {
+        if (src.mode == 0)
+            wgrad_rows<0, false>(R, out, dy, ldy, src, o, i, kq, q0, q1, acc, ds);
+        else if (src.keep)
+            wgrad_rows<1, true>(R, out, dy, ldy, src, o, i, kq, q0, q1, acc, ds);
+        else
+            wgrad_rows<1, false>(R, out, dy, ldy, src, o, i, kq, q0, q1, acc, ds);
     }
     part[w][lane] = acc;
     dpart[w][lane] = ds;
@@ -222,13 +257,19 @@ extern "C" int32_t swarm_wgrad(int64_t rows, int32_t out, const float* dy, int64
         const swarm_wgrad_src_t& s = src[k];
         if (s.in < 1 || (rows > 0 && !s.x) || !s.dw || (s.mode != 0 && s.mode != 1)) return SWARM_ERR_ARG;
         if (s.mode == 0 && s.ld < s.in) return SWARM_ERR_ARG;
-        if (s.mode == 1 && (s.T < 1 || (rows > 0 && !s.h0) || s.ld < s.in || rows % s.T)) return SWARM_ERR_ARG;
+        if (s.mode == 1 && (s.T < 1 || (rows > 0 && !s.h0) || s.ld < s.in || rows % s.T || rows > 0x7fffffff))
+        return SWARM_ERR_ARG;
         S.s[k] = s;
         if (k == 0) S.tiles0 = (s.in + 15) / 16;
         tiles += (s.in + 15) / 16;
     }
     if (n_src == 1) S.s[1] = S.s[0];
     if (rows > 0 && !dy) return SWARM_ERR_ARG;
+    // 32-bit element offsets in the kernel
+    if (rows * ldy >= 0x7fffffffLL) return SWARM_ERR_ARG;
+    for (int k = 0; k < n_src; ++k)
+        if (rows * src[k].ld >= 0x7fffffffLL || (int64_t)(rows / (src[k].mode == 1 ? src[k].T : 1)) * src[k].in >= 0x7fffffffLL)
+            return SWARM_ERR_ARG;
     const int otiles = (out + 15) / 16;
     if ((int64_t)tiles * otiles > 0x7fffffff || otiles > 65535) return SWARM_ERR_ARG;
     wgrad_kernel<<<dim3((unsigned)tiles, (unsigned)otiles), 64 * kWgWaves, 0, static_cast<hipStream_t>(stream)>>>(
