@@ -79,6 +79,14 @@ int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, 
 int32_t swarm_lstm_cell(int64_t n, int32_t units, const float* gates, const float* c_prev, float* h_out,
                         float* c_out, void* stream);
 
+/* Backward of swarm_lstm_cell (the update's one-step recurrences under autograd, reference
+ * poca_networks.py:85-113 nn.LSTM as trained by learned_option_critic_trainer.py:1140-1169): from the
+ * forward's gates, c_prev and c_out and the output gradients dh, dc ([n][units]; either may be NULL =
+ * zero) -> dgates [n][4 units] (gate order i, f, g, o) and dc_prev [n][units]. */
+int32_t swarm_lstm_cell_backward(int64_t n, int32_t units, const float* gates, const float* c_prev,
+                                 const float* c_out, const float* dh, const float* dc, float* dgates, float* dc_prev,
+                                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -69,7 +69,8 @@ class GatherField(C.Structure):
 
 
 # Every symbol include/swarmcritic.h declares (fused critic attention, same library).
-CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_pool_focal", "swarm_rsa_embedding_norm", "swarm_lstm_cell"]
+CRITIC_EXPORTS = ["swarm_rsa_pool", "swarm_rsa_pool_focal", "swarm_rsa_embedding_norm", "swarm_lstm_cell",
+                  "swarm_lstm_cell_backward"]
 TRAIN_EXPORTS = ["swarm_lstm_seq_forward", "swarm_lstm_seq_backward", "swarm_rsa_attn_forward",
                  "swarm_rsa_attn_backward", "swarm_tensor_list_copy", "swarm_lstm_seq_forward_batch",
                  "swarm_lstm_seq_backward_batch", "swarm_row_norm_forward", "swarm_row_norm_backward",
@@ -179,6 +180,8 @@ def load() -> C.CDLL:
     lib.swarm_rsa_embedding_norm.argtypes = [C.c_int64, i32, vp, vp, vp]
     lib.swarm_lstm_cell.restype = i32
     lib.swarm_lstm_cell.argtypes = [C.c_int64, i32, vp, vp, vp, vp, vp]
+    lib.swarm_lstm_cell_backward.restype = i32
+    lib.swarm_lstm_cell_backward.argtypes = [C.c_int64, i32, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.swarm_lstm_seq_forward.restype = i32
     lib.swarm_lstm_seq_forward.argtypes = [C.c_int64, i32, i32] + [vp] * 9
     lib.swarm_lstm_seq_backward.restype = i32

@@ -557,6 +557,41 @@ def lstm_sequences(items):
 SINGLE_STEP_ROWS = 512
 
 
+class _LSTMCell(torch.autograd.Function):
+    """c1 = sigmoid(f) c0 + sigmoid(i) tanh(g), h1 = sigmoid(o) tanh(c1) from the gate pre-activations
+    (n, 4U) in ONE kernel each way (swarm_lstm_cell / swarm_lstm_cell_backward) instead of torch's
+    ~9 elementwise kernels forward and ~15 backward; a missing output gradient stays unmaterialised."""
+
+    @staticmethod
+    def forward(ctx, gates, c0):
+        gates, c0 = gates.contiguous(), c0.contiguous()
+        n, units = c0.shape
+        h1, c1 = torch.empty_like(c0), torch.empty_like(c0)
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(gates.device).cuda_stream)
+        _native.check(lib.swarm_lstm_cell(n, units, _ptr(gates), _ptr(c0), _ptr(h1), _ptr(c1), stream),
+                      "swarm_lstm_cell")
+        ctx.save_for_backward(gates, c0, c1)
+        ctx.set_materialize_grads(False)
+        return h1, c1
+
+    @staticmethod
+    def backward(ctx, dh, dc):
+        gates, c0, c1 = ctx.saved_tensors
+        n, units = c0.shape
+        dgates, dc0 = torch.empty_like(gates), torch.empty_like(c0)
+        dh = dh.contiguous() if dh is not None else None
+        dc = dc.contiguous() if dc is not None else None
+        lib = _native.load()
+        stream = C.c_void_p(torch.cuda.current_stream(gates.device).cuda_stream)
+        _native.check(lib.swarm_lstm_cell_backward(n, units, _ptr(gates), _ptr(c0), _ptr(c1), _ptr(dh), _ptr(dc),
+                                                   _ptr(dgates), _ptr(dc0), stream), "swarm_lstm_cell_backward")
+        return dgates, dc0
+
+
+FUSED_LSTM_CELL = os.environ.get("SWARM_LSTM_CELL", "1") != "0"
+
+
 def _lstm_single_step(lstm: nn.LSTM, seq: torch.Tensor, state):
     """lstm(seq, state) for T = 1 (nn.LSTM's gate order i, f, g, o). A keep mask acts only
     between steps, so a single step has none to apply."""
@@ -575,6 +610,9 @@ def _lstm_single_step(lstm: nn.LSTM, seq: torch.Tensor, state):
     else:
         gates = torch.addmm(torch.nn.functional.linear(x, lstm.weight_ih_l0, lstm.bias_ih_l0 + lstm.bias_hh_l0),
                             h0, lstm.weight_hh_l0.t())
+    if FUSED_LSTM_CELL and seq.is_cuda and gates.dtype == torch.float32:
+        h1, c1 = _LSTMCell.apply(gates, state[1].reshape(n, units))
+        return h1.view(n, 1, units), (h1.view(1, n, units), c1.view(1, n, units))
     i, f, g, o = gates.chunk(4, dim=1)
     c1 = torch.sigmoid(f) * state[1].reshape(n, units) + torch.sigmoid(i) * torch.tanh(g)
     h1 = torch.sigmoid(o) * torch.tanh(c1)

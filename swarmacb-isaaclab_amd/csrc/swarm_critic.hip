@@ -772,6 +772,36 @@ __global__ void __launch_bounds__(256) lstm_cell_kernel(int64_t n, int units, co
     h_out[j] = og * tanhf(c);
 }
 
+// Backward of lstm_cell_kernel for the update's one-step recurrences (autograd, poca_networks
+// _LSTMCell): the gate activations are recomputed from the pre-activations (as the forward), then
+//   dc = dc_out + dh o (1 - tanh(c)^2);  d(pre i, f, g, o) = dc g i (1 - i), dc c_prev f (1 - f),
+//   dc i (1 - g^2), dh tanh(c) o (1 - o);  dc_prev = dc f.
+// dh / dc may be null (no gradient reached that output).
+__global__ void __launch_bounds__(256) lstm_cell_bwd_kernel(int64_t n, int units, const float* __restrict__ gates,
+                                                            const float* __restrict__ c_prev,
+                                                            const float* __restrict__ c_out,
+                                                            const float* __restrict__ dh, const float* __restrict__ dc,
+                                                            float* __restrict__ dgates, float* __restrict__ dc_prev) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= n * units) return;
+    const int64_t row = j / units;
+    const int u = (int)(j - row * units);
+    const float* g = gates + row * 4 * units + u;
+    const float ig = 1.0f / (1.0f + expf(-g[0]));
+    const float fg = 1.0f / (1.0f + expf(-g[units]));
+    const float gg = tanhf(g[2 * units]);
+    const float og = 1.0f / (1.0f + expf(-g[3 * units]));
+    const float tc = tanhf(c_out[j]);
+    const float dhj = dh ? dh[j] : 0.0f;
+    const float dcj = (dc ? dc[j] : 0.0f) + dhj * og * (1.0f - tc * tc);
+    float* d = dgates + row * 4 * units + u;
+    d[0] = dcj * gg * (ig * (1.0f - ig));
+    d[units] = dcj * c_prev[j] * (fg * (1.0f - fg));
+    d[2 * units] = dcj * ig * (1.0f - gg * gg);
+    d[3 * units] = dhj * tc * (og * (1.0f - og));
+    dc_prev[j] = dcj * fg;
+}
+
 int g_cus = 0;
 
 }  // namespace
@@ -860,6 +890,19 @@ int32_t swarm_rsa_embedding_norm(int64_t rows, int32_t hidden, const float* in, 
     if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
     embedding_norm_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(
         rows, reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out));
+    return swarm::record_hip_status();
+}
+
+int32_t swarm_lstm_cell_backward(int64_t n, int32_t units, const float* gates, const float* c_prev,
+                                 const float* c_out, const float* dh, const float* dc, float* dgates, float* dc_prev,
+                                 void* stream) {
+    if (n < 0 || units < 1) return SWARM_ERR_ARG;
+    if (n == 0) return SWARM_OK;
+    if (!gates || !c_prev || !c_out || !dgates || !dc_prev) return SWARM_ERR_ARG;
+    const int64_t blocks = (n * units + 255) / 256;
+    if (blocks > 0x7fffffff) return SWARM_ERR_ARG;
+    lstm_cell_bwd_kernel<<<(unsigned)blocks, 256, 0, static_cast<hipStream_t>(stream)>>>(n, units, gates, c_prev,
+                                                                                       c_out, dh, dc, dgates, dc_prev);
     return swarm::record_hip_status();
 }
 

@@ -103,3 +103,24 @@ def test_lstm_batch_rejects_bad_counts(gpu_device):
     assert lib.swarm_lstm_seq_forward_batch(0, 8, 64, None, None) == -1
     assert lib.swarm_lstm_seq_forward_batch(_native.LSTM_MAX_BATCH + 1, 8, 64, None, None) == -1
     assert lib.swarm_lstm_seq_backward_batch(1, 8, 65, None, None) == -1
+
+
+@pytest.mark.parametrize("n,inp,units", [(2048, 128, 64), (12288, 512, 32), (513, 24, 64)])
+def test_lstm_single_step_fused_cell_matches_torch(gpu_device, n, inp, units):
+    """_lstm_single_step with the fused cell (swarm_lstm_cell / _backward) against nn.LSTM for one
+    step: h1, c1 and every gradient (x, h0, c0, W_ih, W_hh, both biases), with c1 unused (its
+    gradient unmaterialised) and used."""
+    lstm, x, h0, c0, _, _ = _case(n, 1, inp, units, False, gpu_device, seed=n)
+    params = list(lstm.parameters())
+    for use_c in (False, True):
+        xs, hs, cs = (t.clone().requires_grad_(True) for t in (x, h0, c0))
+        out, (h1, c1) = PN._lstm_single_step(lstm, xs, (hs, cs))
+        loss = (out.square()).sum() + ((c1 * 0.5).sum() if use_c else 0.0)
+        g = torch.autograd.grad(loss, [xs, hs, cs] + params)
+        xr, hr, cr = (t.clone().requires_grad_(True) for t in (x, h0, c0))
+        out_r, (h1_r, c1_r) = lstm(xr, (hr, cr))
+        loss_r = (out_r.square()).sum() + ((c1_r * 0.5).sum() if use_c else 0.0)
+        g_r = torch.autograd.grad(loss_r, [xr, hr, cr] + params)
+        assert torch.allclose(out, out_r, **TOL) and torch.allclose(c1, c1_r, **TOL)
+        for a, b in zip(g, g_r):
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-4), float((a - b).abs().max())
