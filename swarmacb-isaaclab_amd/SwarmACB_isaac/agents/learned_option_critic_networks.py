@@ -300,6 +300,85 @@ class LearnedOptionActor(nn.Module):
         next_state = self._pack_state(next_manager_state, next_option_state, B)
         return selector_logits, option_values, termination_logits, action_means, action_stds, attentions, next_state
 
+    # The stages of several independent streams (the update's sequence pass and its next-state pass)
+    # with every per-row layer - manager, attention and option encoders, attention head - as ONE call
+    # over the streams' concatenated rows: one GEMM each way and one weight gradient per layer instead
+    # of one per stream plus the accumulation of the streams' gradients (the recurrences and the
+    # option heads stay per stream).
+    def manager_stages(self, streams):
+        """[manager_stage(obs_seq, state) for each (obs_seq, state) stream]."""
+        if len(streams) == 1:
+            return [self.manager_stage(*streams[0])]
+        mobs, keep, sizes = [], [], []
+        for obs_seq, state in streams:
+            if obs_seq.ndim != 3 or obs_seq.shape[-1] != self.obs_dim:
+                raise ValueError(f"Expected observations (batch, time, {self.obs_dim}), got {tuple(obs_seq.shape)}")
+            B, T = obs_seq.shape[:2]
+            if state is None:
+                state = self.initial_state(B, obs_seq.device)
+            manager_state, option_state = self._unpack_state(state, B)
+            mobs.append((obs_seq[..., 16:20] if self.obs_dim == 24 else obs_seq).reshape(-1, self.manager_obs_dim))
+            keep.append((obs_seq, manager_state, option_state))
+            sizes.append(B * T)
+        enc = self.manager_encoder(torch.cat(mobs))
+        out = []
+        for (obs_seq, manager_state, option_state), part in zip(keep, enc.split(sizes)):
+            B, T = obs_seq.shape[:2]
+            out.append(((self.manager_lstm, part.view(B, T, -1), manager_state, None), (obs_seq, option_state)))
+        return out
+
+    def option_stages(self, ctxs, manager_outs):
+        """[option_stage(ctx, manager_out) for each stream]; the contexts also carry the merged
+        option-encoder output for head_stages."""
+        if len(ctxs) == 1:
+            return [self.option_stage(ctxs[0], manager_outs[0])]
+        O, D, H, mh = self.num_options, self.obs_dim, self.option_hidden, self.manager_hidden_size
+        sizes = [c[0].shape[0] * c[0].shape[1] for c in ctxs]
+        obs_all = torch.cat([c[0].reshape(-1, D) for c in ctxs])
+        sensor_context = self.attention_encoder(obs_all)
+        mf = torch.cat([m[0].reshape(-1, mh) for m in manager_outs])
+        att = torch.sigmoid(self.attention_head(mf + sensor_context)).view(-1, O, D)
+        prod = obs_all.unsqueeze(-2) * att
+        metas, opt_in = [], []
+        for (obs_seq, option_state), (_mf, next_manager_state), a_k, p_k in zip(ctxs, manager_outs, att.split(sizes),
+                                                                               prod.split(sizes)):
+            B, T = obs_seq.shape[:2]
+            metas.append((B, T, a_k.view(B, T, O, D), option_state, next_manager_state))
+            opt_in.append(p_k.view(B, T, O, D).permute(0, 2, 1, 3).reshape(B * O * T, D))
+        enc = self.option_sensor_encoder(torch.cat(opt_in))
+        out = []
+        for (B, T, attentions, option_state, next_manager_state), part in zip(metas, enc.split([B * O * T for B, T, *_
+                                                                                              in metas])):
+            option_enc = part.view(B * O, T, H)
+            out.append(((self.option_lstm, option_enc, option_state, None),
+                        (B, T, attentions, option_enc, next_manager_state, enc)))
+        return out
+
+    def head_stages(self, ctxs, option_outs, with_state=None):
+        """[head_stage(ctx, option_out) for each stream] with the option output encoder as one call;
+        with_state[k] False: stream k's packed next state is not formed (None)."""
+        if len(ctxs) == 1 and len(ctxs[0]) == 5:
+            return [self.head_stage(ctxs[0], option_outs[0])]
+        O, H, R = self.num_options, self.option_hidden, self.option_recurrent_size
+        enc_all = ctxs[0][5]
+        rec_all = torch.cat([o[0].reshape(-1, R) for o in option_outs])
+        feats = self.option_output_encoder(torch.cat([enc_all, rec_all], dim=-1))
+        kinds = self._head_kinds()
+        stacked = self._stacked_heads()
+        out = []
+        for k, ((B, T, attentions, _enc, next_manager_state, _all), (_rec, next_option_state), part) in enumerate(
+                zip(ctxs, option_outs, feats.split([c[0] * O * c[1] for c in ctxs]))):
+            option_features = part.view(B, O, T, H).permute(0, 2, 1, 3)
+            heads = _option_heads(kinds, option_features, stacked)
+            option_values, action_means, termination_logits = heads[0].squeeze(-1), heads[1], heads[2].squeeze(-1)
+            selector_logits = heads[3].squeeze(-1) if self.separate_selector else option_values
+            action_stds = self.option_log_stds().exp().view(1, 1, O, self.act_dim).expand_as(action_means)
+            keep_state = with_state is None or with_state[k]
+            next_state = self._pack_state(next_manager_state, next_option_state, B) if keep_state else None
+            out.append((selector_logits, option_values, termination_logits, action_means, action_stds, attentions,
+                        next_state))
+        return out
+
     def step(self, obs: torch.Tensor, state=None):
         out = self.forward_sequence(obs.unsqueeze(1), state)
         return tuple(x[:, 0] for x in out[:6]) + (out[6],)

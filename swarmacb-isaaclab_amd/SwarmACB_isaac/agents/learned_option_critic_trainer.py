@@ -547,17 +547,24 @@ class LearnedOptionCriticTrainer(TrainerBase):
             (self.option_critic, flat_states, encoded, focal_ids,
              {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")}, L,
              ("joint", "baseline"))]
-        a_item, a_ctx = self.actor.manager_stage(obs, mem0)
+        # the actor's sequence pass and its next-state pass (termination logits at s' from the stored
+        # post-decision memory, LOT:1140-1169) as two streams of one forward: their per-row layers run
+        # once over both streams' rows, the recurrences per stream
+        next_h = batch["next_memory_h"].reshape(B * L, -1).unsqueeze(0).detach()
+        next_c = batch["next_memory_c"].reshape(B * L, -1).unsqueeze(0).detach()
+        (a_item, a_ctx), (n_item, n_ctx) = self.actor.manager_stages(
+            [(obs, mem0), (next_obs.reshape(B * L, 1, self.obs_dim), (next_h, next_c))])
         with torch.no_grad():
             r_item, r_ctx = reference_actor.manager_stage(obs, (batch["memory_h"].unsqueeze(0),
                                                                 batch["memory_c"].unsqueeze(0)))
-        outs = lstm_sequences([a_item, r_item + (True,)])
-        a_item, a_ctx = self.actor.option_stage(a_ctx, outs[0])
+        outs = lstm_sequences([a_item, r_item + (True,), n_item])
+        (a_item, a_ctx), (n_item, n_ctx) = self.actor.option_stages([a_ctx, n_ctx], [outs[0], outs[2]])
         with torch.no_grad():
             r_item, r_ctx = reference_actor.option_stage(r_ctx, outs[1])
-        opt_outs = lstm_sequences([a_item, r_item + (True,)])
-        (_sel, option_values, _term, action_means, action_stds, attentions,
-         _next) = self.actor.head_stage(a_ctx, opt_outs[0])
+        opt_outs = lstm_sequences([a_item, r_item + (True,), n_item])
+        seq_out, next_out = self.actor.head_stages([a_ctx, n_ctx], [opt_outs[0], opt_outs[2]],
+                                                   with_state=(False, False))
+        (_sel, option_values, _term, action_means, action_stds, attentions, _next) = seq_out
         with torch.no_grad():
             ref_out = reference_actor.head_stage(r_ctx, opt_outs[1])
             ref_means, ref_stds = ref_out[3], ref_out[4]
@@ -609,10 +616,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
             denom=n_mask_f * A if d_mask is not None else None)
 
         # termination logits at s' from the stored post-decision memory (LOT:1140-1169)
-        next_h = batch["next_memory_h"].reshape(B * L, -1).unsqueeze(0).detach()
-        next_c = batch["next_memory_c"].reshape(B * L, -1).unsqueeze(0).detach()
-        (_s, next_option_values, next_term_logits, _m, _sd, _a, _n) = self.actor.step(
-            next_obs.reshape(B * L, self.obs_dim), (next_h, next_c))
+        next_option_values, next_term_logits = next_out[1][:, 0], next_out[2][:, 0]
         next_beta_logits = self.actor.selected_termination_logits(next_term_logits, options.reshape(-1)).view(B, L)
 
         flat_returns = batch["returns"].reshape(-1)
