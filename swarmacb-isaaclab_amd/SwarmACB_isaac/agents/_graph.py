@@ -95,8 +95,11 @@ class GraphedStep:
             self.reset(key)
         sig = self.signature(batch)
         if self.graph is not None and sig == self.sig:
-            for k, v in batch.items():
-                self.static[k].copy_(v)
+            if hasattr(batch, "gather_into") and batch.keys() == self.static.keys():
+                batch.gather_into(self.static)   # one gather launch into the static inputs
+            else:
+                for k, v in batch.items():
+                    self.static[k].copy_(v)
             self.graph.replay()
             self.replays += 1
             return self.out

@@ -86,24 +86,34 @@ def _row_shape(src: torch.Tensor, kind: str) -> tuple:
 
 
 def gather(mode: int, spec, arrays: dict, order: torch.Tensor, *, chunks=None, n_items: int, L: int = 1,
-           T: int, E: int, N: int) -> dict:
+           T: int, E: int, N: int, out: dict | None = None) -> dict:
     """Gather B = len(order) rows of every field of `spec` in one launch.
 
     spec: [(key, attr, kind)]; arrays[attr] is a buffer tensor (T_cap, E[, N], ...).
-    mode 0 = padded sequences (chunk table), mode 1 = flat focal-agent rows."""
+    mode 0 = padded sequences (chunk table), mode 1 = flat focal-agent rows.
+    out: preallocated contiguous destinations by key (e.g. a captured step's static inputs)."""
     dev = order.device
     B = order.numel()
     if order.dtype != torch.int64:
         raise ValueError("order must be int64")
+    given = out
     out = {}
+
+    def dest(key, shape, dtype):
+        if given is None:
+            return torch.empty(shape, dtype=dtype, device=dev)
+        t = given[key]
+        if tuple(t.shape) != tuple(shape) or t.dtype != dtype or not t.is_contiguous():
+            raise ValueError(f"gather: destination {key} is {tuple(t.shape)} {t.dtype}, expected {tuple(shape)} {dtype}")
+        return t
     fields = []
     mask = ids = None
     for key, attr, kind in spec:
         if kind == IDS:
-            ids = out[key] = torch.empty(B, dtype=torch.int64, device=dev)
+            ids = out[key] = dest(key, (B,), torch.int64)
             continue
         if kind == MASK:
-            mask = out[key] = torch.empty(B, L, dtype=torch.float32, device=dev)
+            mask = out[key] = dest(key, (B, L), torch.float32)
             continue
         src = arrays[attr]
         _dev_check(src)
@@ -112,7 +122,7 @@ def gather(mode: int, spec, arrays: dict, order: torch.Tensor, *, chunks=None, n
         row = _row_shape(src, kind)
         words = math.prod(row) * src.element_size() // 4
         seq = mode == 0 and kind in (FOCAL, GROUP)
-        dst = torch.empty((B, L) + row if seq else (B,) + row, dtype=src.dtype, device=dev)
+        dst = dest(key, (B, L) + row if seq else (B,) + row, src.dtype)
         out[key] = dst
         fields.append(_native.GatherField(src.data_ptr(), dst.data_ptr(), words, _native.GATHER_KINDS[kind]))
     if len(fields) > _native.GATHER_MAX_FIELDS:
@@ -150,8 +160,24 @@ def windowed(spec, arrays, order, starts, per_batch, bytes_per_row, *, mode, bud
             big.update(gather(mode, extra[0], extra[1], order[lo:hi], **dict(kw, chunks=extra[2])))
         sizes = [min(a + per_batch, n) - a for a in group]
         parts = [(k, v.split(sizes)) for k, v in big.items()]  # one view per batch, made in C++
-        for j in range(len(group)):
-            yield {k: p[j] for k, p in parts}
+        for j, a in enumerate(group):
+            yield Minibatch({k: p[j] for k, p in parts}, mode, spec, arrays, order[a:a + sizes[j]], extra, kw)
+
+
+class Minibatch(dict):
+    """A minibatch's tensors (views of its window's gather) that can also gather themselves again
+    straight into given destinations: a replayed optimizer step's static inputs are filled by ONE
+    gather launch (two with chunk-start storage) instead of one copy per field (agents/_graph.py)."""
+
+    def __init__(self, tensors, mode, spec, arrays, order, extra, kw):
+        super().__init__(tensors)
+        self._regather = (mode, spec, arrays, order, extra, kw)
+
+    def gather_into(self, out: dict) -> None:
+        mode, spec, arrays, order, extra, kw = self._regather
+        gather(mode, spec, arrays, order, out=out, **kw)
+        if extra is not None:
+            gather(mode, extra[0], extra[1], order, out=out, **dict(kw, chunks=extra[2]))
 
 
 def row_bytes(spec, arrays, L: int, mode: int) -> int:
