@@ -709,9 +709,52 @@ class LearnedOptionCriticTrainer(TrainerBase):
     def compute_losses(self, batch: dict, current_eps: float, reference_actor=None) -> dict:
         return self._compute_sequence_losses(batch, current_eps, reference_actor or self.reference_actor)
 
+    def _objective_coefs(self):
+        """(actor term names, their loss names, coefficients; critic loss names, coefficients) of
+        learned_option_critic_trainer.py:1531-1581 at the current schedule values."""
+        cfg = self.cfg
+        actor = [("objective_intra_option", "intra_option_loss", cfg.intra_option_coef),
+                 ("objective_selector", "selector_loss", cfg.selector_coef),
+                 ("objective_local_option_value", "local_option_value_loss", cfg.local_option_value_coef),
+                 ("objective_termination", "termination_loss", cfg.termination_coef),
+                 ("objective_termination_prior", "termination_prior_loss", self.current_termination_prior_coef),
+                 ("objective_option_balance", "option_balance_loss", self.current_option_balance_coef),
+                 ("objective_attention_diversity", "attention_diversity_loss", cfg.attention_diversity_coef),
+                 ("objective_attention_temporal", "attention_temporal_loss", cfg.attention_temporal_coef),
+                 ("objective_action_entropy", "action_entropy", -self.current_beta),
+                 ("objective_option_entropy", "option_entropy", -cfg.option_entropy_coef),
+                 ("objective_termination_entropy", "termination_entropy", -cfg.termination_entropy_coef)]
+        critic = [("value_loss", cfg.value_coef), ("action_baseline_loss", cfg.action_baseline_coef),
+                  ("joint_option_value_loss", cfg.option_value_coef), ("option_baseline_loss", cfg.option_baseline_coef)]
+        return actor, critic
+
+    def _stage_objective_coefs(self, device):
+        """The coefficients as one device vector, made outside any graph capture (a host -> device
+        copy cannot be captured); objectives() then forms both losses in a few launches."""
+        actor, critic = self._objective_coefs()
+        vals = [c for _, _, c in actor] + [c for _, c in critic]
+        cur = self.__dict__.get("_obj_coefs")
+        if cur is None or cur[0] != vals or cur[1].device != device:
+            self.__dict__["_obj_coefs"] = (vals, torch.tensor(vals, dtype=torch.float32, device=device))
+
     def objectives(self, losses: dict):
         """(actor terms dict, actor loss, critic loss) of learned_option_critic_trainer.py:1531-1581."""
         cfg = self.cfg
+        actor, critic = self._objective_coefs()
+        staged = self.__dict__.get("_obj_coefs")
+        ref = losses["intra_option_loss"]
+        if (staged is not None and staged[0] == [c for _, _, c in actor] + [c for _, c in critic]
+                and staged[1].device == ref.device
+                and all(losses[n].dtype == torch.float32 and losses[n].numel() == 1
+                        for n in [a for _, a, _ in actor] + [a for a, _ in critic])):
+            # every term as one stacked product: 6 launches instead of ~28 scalar ones (the sums'
+            # order differs from the reference's left-to-right Python sum at fp32 rounding)
+            # (separate products: the actor and critic losses are differentiated one after the other)
+            na = len(actor)
+            ta = torch.stack([losses[a].reshape(()) for _, a, _ in actor]) * staged[1][:na]
+            tc = torch.stack([losses[a].reshape(()) for a, _ in critic]) * staged[1][na:]
+            terms = {name: ta[i] for i, (name, _, _) in enumerate(actor)}
+            return terms, ta.sum(), tc.sum()
         terms = {
             "objective_intra_option": cfg.intra_option_coef * losses["intra_option_loss"],
             "objective_selector": cfg.selector_coef * losses["selector_loss"],
@@ -862,6 +905,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
                        "apply_u8": torch.zeros((), dtype=torch.uint8, device=dev)}
         for t in self._g.values():
             t.zero_()
+        self._stage_objective_coefs(dev)
         self._init_adam_state(self.actor_optimizer)
         self._init_adam_state(self.critic_optimizer)
         if dev.type == "cuda":
@@ -933,6 +977,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         actor_early_stopped = False
         self.reference_actor.load_state_dict(self.actor.state_dict())
         self.reference_actor.eval()
+        self._stage_objective_coefs(dev)   # eager and graphed steps form the losses alike
         if self._graphs_ok():
             (totals, grad_norms, samples, num_batches, actor_updates, critic_updates, max_policy_kl, max_action_kl,
              max_option_kl, initial_policy_kl, actor_early_stopped) = self._update_graphed()

@@ -334,8 +334,9 @@ class _LSTMSequences(torch.autograd.Function):
                       "swarm_lstm_seq_forward_batch")
         for i in range(k):
             h_out, c_out = saved[7 * i + 4], saved[7 * i + 5]
-            outs += [h_out, c_out[:, -1].contiguous()]     # after the launch that writes c_out
+            outs += [h_out, c_out[:, -1]]     # the final cell state: a view (after the launch that writes c_out)
         ctx.k = k
+        ctx.set_materialize_grads(False)   # an unused final state (the update's) gets no zero-filled gradient
         ctx.save_for_backward(*saved)
         return tuple(outs)
 
@@ -351,7 +352,8 @@ class _LSTMSequences(torch.autograd.Function):
         descs, res, keepalive = [], {}, []
         for i in live:
             w_hh, h0, c0, keep, h_out, c_out, act = saved[7 * i:7 * i + 7]
-            dh_out, dc_n = grads[2 * i].contiguous(), grads[2 * i + 1].contiguous()
+            dh_out = grads[2 * i].contiguous() if grads[2 * i] is not None else torch.zeros_like(h_out)
+            dc_n = grads[2 * i + 1].contiguous() if grads[2 * i + 1] is not None else None
             dxg = torch.empty_like(act)
             dh0, dc0 = torch.empty_like(h0), torch.empty_like(c0)
             descs.append(_native.LstmSeqBwd(h_out.shape[0], _addr(w_hh), _addr(c0), _addr(keep), _addr(c_out),

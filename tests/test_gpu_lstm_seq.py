@@ -121,6 +121,8 @@ def test_lstm_single_step_fused_cell_matches_torch(gpu_device, n, inp, units):
         out_r, (h1_r, c1_r) = lstm(xr, (hr, cr))
         loss_r = (out_r.square()).sum() + ((c1_r * 0.5).sum() if use_c else 0.0)
         g_r = torch.autograd.grad(loss_r, [xr, hr, cr] + params)
-        assert torch.allclose(out, out_r, **TOL) and torch.allclose(c1, c1_r, **TOL)
+        # the gate GEMMs differ from MIOpen's in their reduction order over inp + units terms (up to
+        # 544 at the option LSTM's shape): fp32 tolerance of that depth
+        assert torch.allclose(out, out_r, rtol=1e-4, atol=1e-5) and torch.allclose(c1, c1_r, rtol=1e-4, atol=1e-5)
         for a, b in zip(g, g_r):
             assert torch.allclose(a, b, rtol=1e-4, atol=1e-4), float((a - b).abs().max())
