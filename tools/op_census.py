@@ -33,6 +33,10 @@ class Census(TorchDispatchMode):
                 if "SwarmACB_isaac" in fr.filename:
                     site = f"{os.path.basename(fr.filename)}:{fr.lineno} {fr.name}"
                     break
+            if site == "?":
+                node = torch._C._current_autograd_node()   # backward: the autograd node running
+                if node is not None:
+                    site = f"<backward> {node.name()}"
             self.count[(name, site)] += 1
         return func(*args, **(kwargs or {}))
 
