@@ -105,16 +105,10 @@ template <int KU>
 __device__ __forceinline__ float row_dot_lds(const float (&w)[KU], const float* v) {
     static_assert(KU % 4 == 0, "packed chains need KU % 4 == 0");
     const float4* v4 = reinterpret_cast<const float4*>(v);
-    // every read of the row first, then the chains: with the reads interleaved the compiler
-    // cycled three register quads through them, i.e. ~5 dependent LDS round trips per step
-    float4 hv[KU / 4];
-#pragma unroll
-    for (int k = 0; k < KU / 4; ++k) hv[k] = v4[k];
-    __builtin_amdgcn_sched_barrier(0);
     f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
 #pragma unroll
     for (int k = 0; k < KU; k += 4) {
-        const float4 h = hv[k / 4];
+        const float4 h = v4[k / 4];
         a01 = __builtin_elementwise_fma((f32x2){w[k], w[k + 1]}, (f32x2){h.x, h.y}, a01);
         a23 = __builtin_elementwise_fma((f32x2){w[k + 2], w[k + 3]}, (f32x2){h.z, h.w}, a23);
     }
