@@ -86,11 +86,6 @@ __device__ __forceinline__ float act_tanh(float x) {
     return copysignf(ax < 0.625f ? small : big, x);
 }
 
-// lane k's value of v, in a scalar register (v_readlane_b32 on the bit pattern)
-__device__ __forceinline__ float lane_bcast(float v, int k) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
-}
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void wave_sync() {
@@ -105,10 +100,16 @@ template <int KU>
 __device__ __forceinline__ float row_dot_lds(const float (&w)[KU], const float* v) {
     static_assert(KU % 4 == 0, "packed chains need KU % 4 == 0");
     const float4* v4 = reinterpret_cast<const float4*>(v);
+    // every read of the row first, then the chains: with the reads interleaved the compiler
+    // cycled three register quads through them, i.e. ~5 dependent LDS round trips per step
+    float4 hv[KU / 4];
+#pragma unroll
+    for (int k = 0; k < KU / 4; ++k) hv[k] = v4[k];
+    __builtin_amdgcn_sched_barrier(0);
     f32x2 a01 = {0.0f, 0.0f}, a23 = {0.0f, 0.0f};
 #pragma unroll
     for (int k = 0; k < KU; k += 4) {
-        const float4 h = v4[k / 4];
+        const float4 h = hv[k / 4];
         a01 = __builtin_elementwise_fma((f32x2){w[k], w[k + 1]}, (f32x2){h.x, h.y}, a01);
         a23 = __builtin_elementwise_fma((f32x2){w[k + 2], w[k + 3]}, (f32x2){h.z, h.w}, a23);
     }
@@ -214,6 +215,7 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
     __shared__ __attribute__((aligned(16))) float dgs[4 * MAXU];
     __shared__ __attribute__((aligned(16))) float part[4 * MAXU];
     __shared__ __attribute__((aligned(16))) float partb[2][4 * MAXU];   // UC == MAXU path
+    __shared__ __attribute__((aligned(16))) float gqs[NT / 64][MAXU];    // UC == MAXU: each wave's gate gradients
     const int item = batch_item(bt, blockIdx.x);
     const BwdSeq& sq = bt.s[item];
     const float* __restrict__ w_hh = sq.w_hh;
@@ -303,19 +305,12 @@ __global__ void __launch_bounds__(NT) lstm_seq_bwd_kernel(int T, int U_rt, const
                 dc_prev = dc * in.fg;
                 dc_rec = dc_prev * in.kprev;
                 k_after = in.kprev;
-                float gk[KU];
-#pragma unroll
-                for (int m = 0; m < KU; ++m) gk[m] = lane_bcast(gq, m);
-                __builtin_amdgcn_sched_barrier(0);
-                float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-#pragma unroll
-                for (int m = 0; m < KU; m += 4) {
-                    s0 = fmaf(wt[m], gk[m], s0);
-                    s1 = fmaf(wt[m + 1], gk[m + 1], s1);
-                    s2 = fmaf(wt[m + 2], gk[m + 2], s2);
-                    s3 = fmaf(wt[m + 3], gk[m + 3], s3);
-                }
-                partb[t & 1][j] = (s0 + s1) + (s2 + s3);
+                // the wave's 64 gate gradients as one LDS row, read back as same-address float4
+                // broadcasts (all in flight at once) into packed FMAs: the same four residue
+                // chains (s0 + s1) + (s2 + s3) as 64 v_readlane_b32 + scalar FMAs, bitwise
+                gqs[q][u] = gq;
+                wave_sync();
+                partb[t & 1][j] = row_dot_lds<KU>(wt, gqs[q]);
                 __syncthreads();
                 continue;
             }
