@@ -827,8 +827,39 @@ class LearnedOptionCriticTrainer(TrainerBase):
             self._rb = rb
         return rb
 
-    def _list_copy(self, dst_ptrs, src_ptrs, unless=None):
-        rb = self._rb
+    def _snapshot_tables(self, live):
+        """swarm_tensor_list_copy tables for the update-start snapshot of `live` (parameters and
+        Adam state of every optimizer): one launch each way instead of one clone per tensor.
+        None when a tensor is not a contiguous 32-bit CUDA tensor (then the caller clones)."""
+        key = tuple(t.data_ptr() for t in live)
+        sn = getattr(self, "_snap", None)
+        if sn is not None and sn["key"] == key:
+            return sn
+        if not live or any(not t.is_cuda or t.element_size() != 4 or not t.is_contiguous() for t in live):
+            return None
+        saved = [torch.empty_like(t) for t in live]
+        i64 = dict(dtype=torch.int64, device=live[0].device)
+        self._snap = {"key": key, "saved": saved, "n": len(live),
+                      "live_ptrs": torch.tensor([t.data_ptr() for t in live], **i64),
+                      "saved_ptrs": torch.tensor([t.data_ptr() for t in saved], **i64),
+                      "words": torch.tensor([t.numel() for t in live], **i64),
+                      "max_words": max(t.numel() for t in live)}
+        return self._snap
+
+    def _sync_reference_actor(self):
+        """reference_actor.load_state_dict(actor.state_dict()) (LOT:1438) as one multi-tensor copy
+        of the parameters and buffers (same module class, same order); load_state_dict when the
+        two disagree in shape."""
+        src = list(self.actor.parameters()) + list(self.actor.buffers())
+        dst = list(self.reference_actor.parameters()) + list(self.reference_actor.buffers())
+        if len(src) == len(dst) and all(s.shape == d.shape and s.dtype == d.dtype for s, d in zip(src, dst)):
+            with torch.no_grad():
+                torch._foreach_copy_(dst, src)
+        else:
+            self.reference_actor.load_state_dict(self.actor.state_dict())
+
+    def _list_copy(self, dst_ptrs, src_ptrs, unless=None, rb=None):
+        rb = self._rb if rb is None else rb
         lib = _native.load()
         stream = C.c_void_p(torch.cuda.current_stream(dst_ptrs.device).cuda_stream)
         ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None   # noqa: E731
@@ -920,13 +951,20 @@ class LearnedOptionCriticTrainer(TrainerBase):
         opts = (self.actor_optimizer, self.critic_optimizer)
         live = list(self.actor_parameters) + list(self.critic_parameters) + \
             [v for o in opts for st in o.state.values() for v in st.values() if torch.is_tensor(v)]
-        with torch.no_grad():
-            saved = [t.detach().clone() for t in live]
+        snap = self._snapshot_tables(live)
+        if snap is not None:
+            self._list_copy(snap["saved_ptrs"], snap["live_ptrs"], rb=snap)
+        else:
+            with torch.no_grad():
+                saved = [t.detach().clone() for t in live]
 
         def fail(exc):
-            with torch.no_grad():
-                for t, b in zip(live, saved):
-                    t.copy_(b)
+            if snap is not None:
+                self._list_copy(snap["live_ptrs"], snap["saved_ptrs"], rb=snap)
+            else:
+                with torch.no_grad():
+                    for t, b in zip(live, saved):
+                        t.copy_(b)
             raise exc
 
         for _epoch in range(cfg.num_epochs):
@@ -975,7 +1013,7 @@ class LearnedOptionCriticTrainer(TrainerBase):
         num_batches = actor_updates = critic_updates = 0
         max_policy_kl = max_action_kl = max_option_kl = initial_policy_kl = 0.0
         actor_early_stopped = False
-        self.reference_actor.load_state_dict(self.actor.state_dict())
+        self._sync_reference_actor()
         self.reference_actor.eval()
         self._stage_objective_coefs(dev)   # eager and graphed steps form the losses alike
         if self._graphs_ok():
@@ -1032,8 +1070,16 @@ class LearnedOptionCriticTrainer(TrainerBase):
         modules = (("actor", self.actor), ("team_critic", self.team_critic), ("action_critic", self.action_critic),
                    ("option_critic", self.option_critic))
         named = [(f"{m}.{n}", p) for m, mod in modules for n, p in mod.named_parameters()]
-        finite = torch.stack([torch.isfinite(p).all() for _, p in named]).tolist()
-        bad = [n for (n, _), ok in zip(named, finite) if not ok]
+        with torch.no_grad():
+            # p * 0 is 0 for every finite element and NaN for an infinite or NaN one, and a
+            # NaN term makes the tensor's norm NaN: one multi-tensor pass and one host read
+            # instead of four launches per parameter; the names only when one fails
+            zn = torch._foreach_norm(torch._foreach_mul([p.detach() for _, p in named], 0.0))
+            all_finite = bool(torch.isfinite(torch.stack(zn)).all())
+        bad = []
+        if not all_finite:
+            finite = torch.stack([torch.isfinite(p).all() for _, p in named]).tolist()
+            bad = [n for (n, _), ok in zip(named, finite) if not ok]
         if bad:
             raise FloatingPointError("LearnedOC optimizer produced non-finite parameters: " + ", ".join(bad[:10]))
         self.update_count += 1

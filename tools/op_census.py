@@ -3,6 +3,8 @@
 line that issued it (a TorchDispatchMode over the trainer's own update; no profiler). Prints the
 ops per step, grouped by (op, innermost SwarmACB_isaac frame), largest counts first.
 Usage (GPU box): SWARM_GRAPHS=0 python tools/op_census.py --config C5 [--steps 4] [--ops cat,copy_,mul]
+       (graphed step: python tools/op_census.py --config C5 --graphed --steps 3: two warm-up steps
+       and the capture, whose ops are what every replay runs; includes the update's own ops)
 """
 import argparse
 import collections
@@ -49,6 +51,8 @@ def main():
     ap.add_argument("--envs", type=int, default=256)
     ap.add_argument("--ops", default="", help="comma-separated aten op names (default: all)")
     ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--graphed", action="store_true", help="count the graphed step's ops: the census covers the "
+                    "step runner's eager warm-up steps and its capture (SWARM_GRAPHS on), --steps of them")
     a = ap.parse_args()
     from SwarmACB_isaac.agents.config import make_env_cfg
     from SwarmACB_isaac.agents.metrics import NullWriter
@@ -68,9 +72,10 @@ def main():
     tr.collect_rollout(obs, a.decisions)
     orig = tr._sequence_batches
     cfg.num_epochs = 1
-    tr._sequence_batches = lambda: itertools.islice(orig(), 2)
-    tr.update()                                  # warm-up (allocator, Adam state)
-    torch.cuda.synchronize()
+    if not a.graphed:
+        tr._sequence_batches = lambda: itertools.islice(orig(), 2)
+        tr.update()                              # warm-up (allocator, Adam state)
+        torch.cuda.synchronize()
     tr._sequence_batches = lambda: itertools.islice(orig(), a.steps)
     ops = set(o for o in a.ops.split(",") if o)
     with Census(ops) as c:
