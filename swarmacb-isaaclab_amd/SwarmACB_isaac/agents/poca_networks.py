@@ -39,7 +39,7 @@ _KERNEL_INITS = {
 
 # rows from which a layer's weight gradient is split over row chunks (A/B: profiles/r04/train/splitk_rows_ab.txt)
 SPLITK_MIN_ROWS = int(os.environ.get("SWARM_SPLITK_MIN_ROWS", "4096"))
-SPLITK_CHUNK_ROWS = 1024   # rows per chunk of that split
+SPLITK_CHUNK_ROWS = int(os.environ.get("SWARM_SPLITK_CHUNK_ROWS", "1024"))   # rows per chunk of that split
 SPLITK_SLAB_ROWS = 256     # rows per column-sum slab of its bias gradient
 # False (or SWARM_SPLITK_SUMS=0): the chunk / bias sums run torch's reductions
 SPLITK_NATIVE_SUMS = os.environ.get("SWARM_SPLITK_SUMS", "1") != "0"
