@@ -1067,6 +1067,14 @@ class LearnedOptionCriticTrainer(TrainerBase):
             raise RuntimeError("OC2 applied no actor updates for this rollout. The frozen reference invariant "
                                "should guarantee at least one safe policy minibatch.")
         check_policy_inputs(self.device)
+        self._check_parameters_finite()
+        self.update_count += 1
+        return self._update_metrics(totals, grad_norms, samples, num_batches, actor_updates, critic_updates,
+                                    max_policy_kl, max_action_kl, max_option_kl, initial_policy_kl,
+                                    actor_early_stopped)
+
+    def _check_parameters_finite(self):
+        """LOT:1642-1658: raise FloatingPointError naming the parameters that hold a non-finite value."""
         modules = (("actor", self.actor), ("team_critic", self.team_critic), ("action_critic", self.action_critic),
                    ("option_critic", self.option_critic))
         named = [(f"{m}.{n}", p) for m, mod in modules for n, p in mod.named_parameters()]
@@ -1082,10 +1090,6 @@ class LearnedOptionCriticTrainer(TrainerBase):
             bad = [n for (n, _), ok in zip(named, finite) if not ok]
         if bad:
             raise FloatingPointError("LearnedOC optimizer produced non-finite parameters: " + ", ".join(bad[:10]))
-        self.update_count += 1
-        return self._update_metrics(totals, grad_norms, samples, num_batches, actor_updates, critic_updates,
-                                    max_policy_kl, max_action_kl, max_option_kl, initial_policy_kl,
-                                    actor_early_stopped)
 
     def _update_metrics(self, totals, grad_norms, samples, num_batches, actor_updates, critic_updates, max_policy_kl,
                         max_action_kl, max_option_kl, initial_policy_kl, actor_early_stopped) -> dict:

@@ -147,3 +147,40 @@ def test_graphed_oc2_update_equals_eager(target_kl, gpu_device, tmp_path, monkey
     print(f"[graph] oc2 target_kl={target_kl}: {tr._graphed.replays} replayed, actor updates "
           f"{graphed_metrics['actor_updates']:.0f}/{graphed_metrics['critic_updates']:.0f}, max param diff {worst:.3g}")
     env.close()
+
+
+def test_graphed_oc2_update_failure_restores_update_start_state(gpu_device, tmp_path, monkeypatch):
+    """A graphed OC2 update whose losses turn non-finite raises after its last replay and restores
+    every parameter and Adam tensor to its update-start value (the snapshot is one list-copy launch
+    each way), as the eager update, which raises before the bad optimizer step, leaves them."""
+    from SwarmACB_isaac.agents import _graph
+    from SwarmACB_isaac.agents.config import LearnedOptionCriticConfig, make_env_cfg
+    from SwarmACB_isaac.agents.learned_option_critic_trainer import LearnedOptionCriticTrainer
+    from SwarmACB_isaac.agents.metrics import NullWriter
+    from SwarmACB_isaac.registry import make
+
+    torch.manual_seed(0)
+    task, variant = "SwarmACB-XOR-v0", "cyclamen"
+    cfg = LearnedOptionCriticConfig(horizon=12, mini_batch_size=256, num_epochs=2, sequence_length=8,
+                                    log_dir=str(tmp_path))
+    env = make(task, make_env_cfg(task, variant, {"num_envs": 32}, cfg.trainer_type, seed=0), device=gpu_device)
+    tr = LearnedOptionCriticTrainer(env, cfg, writer=NullWriter())
+    obs, _ = env.reset()
+    tr.collect_rollout(obs, cfg.horizon)
+    opts = [tr.actor_optimizer, tr.critic_optimizer]
+    _graph.make_capturable(opts, tr.device)
+    tr._init_adam_state(tr.actor_optimizer)
+    tr._init_adam_state(tr.critic_optimizer)
+    monkeypatch.setattr(_graph, "ENABLED", True)
+    T = tr.buffer.ptr
+    tr.buffer.action_advantages[:T] = float("nan")
+    live = list(tr.params) + [v for o in opts for st in o.state.values() for v in st.values() if torch.is_tensor(v)]
+    before = [t.detach().clone() for t in live]
+    # the NaN losses' steps also make the wheel means non-finite: whichever check reports first
+    # (the loss flag or the Normal-argument flag), the update fails through the same restore
+    with pytest.raises((FloatingPointError, ValueError), match="non-finite"):
+        tr.update()
+    assert tr._snap is not None, "the update-start snapshot did not take the list-copy path"
+    for a, b in zip(before, live):
+        assert torch.equal(a, b.detach())
+    env.close()

@@ -100,3 +100,35 @@ def test_oc2_refuses_discrete_or_short_obs():
     with pytest.raises(ValueError, match="24-channel"):
         LearnedOptionCriticTrainer(OF.ReplayEnv(OF.load("oc_update"), "cpu", discrete=False),
                                    LearnedOptionCriticConfig(), writer=NullWriter())
+
+
+@pytest.mark.parametrize("value", [float("inf"), float("-inf"), float("nan")])
+def test_oc2_parameter_check_names_non_finite_parameters(value):
+    """The end-of-update parameter check (one multi-tensor pass) raises exactly when a parameter
+    holds an infinite or NaN element and names it, as the reference's per-parameter loop does;
+    large finite values pass."""
+    tr, _fx, _names, _named = O2.make_oc2_trainer("oc2_update", "cpu")
+    tr._check_parameters_finite()
+    with torch.no_grad():
+        tr.team_critic.value_head.weight.view(-1)[0] = 3.0e38     # squares overflow, still finite
+    tr._check_parameters_finite()
+    with torch.no_grad():
+        tr.action_critic.value_head.bias.view(-1)[0] = value
+    with pytest.raises(FloatingPointError, match=r"action_critic\.value_head\.bias"):
+        tr._check_parameters_finite()
+
+
+def test_oc2_reference_actor_sync_equals_load_state_dict():
+    """update()'s frozen-actor copy (one multi-tensor copy) leaves the reference actor equal to
+    reference_actor.load_state_dict(actor.state_dict()), stacked head storage included."""
+    tr, _fx, _names, _named = O2.make_oc2_trainer("oc2_update", "cpu")
+    with torch.no_grad():
+        for p in tr.actor.parameters():
+            p.add_(torch.randn_like(p))
+    tr._sync_reference_actor()
+    ref = tr.reference_actor.state_dict()
+    for k, v in tr.actor.state_dict().items():
+        assert torch.equal(ref[k], v), k
+    x = torch.randn(2, 3, 24)
+    for a, b in zip(tr.actor.forward_sequence(x)[:6], tr.reference_actor.forward_sequence(x)[:6]):
+        assert torch.equal(a, b)
