@@ -97,6 +97,11 @@ def _option_heads(head_lists, feats: torch.Tensor, stacked=None) -> list[torch.T
     return [t.reshape(*lead, O, n) for t, n in zip(torch.split(y, outs, dim=-1), outs)]
 
 
+class UnpackedState(tuple):
+    """(manager (h, c), option (h, c)): a packed recurrent state already split by _unpack_state,
+    accepted wherever a packed state is (the update's actor and its frozen copy share one split)."""
+
+
 class LearnedOptionActor(nn.Module):
     """Shared recurrent Attention Option-Critic policy of every robot (LON:96-622)."""
 
@@ -232,6 +237,8 @@ class LearnedOptionActor(nn.Module):
         return z, z.clone()
 
     def _unpack_state(self, state, batch_size: int):
+        if isinstance(state, UnpackedState):
+            return state
         h, c = state
         expected = (1, batch_size, self.hidden_size)
         if tuple(h.shape) != expected or tuple(c.shape) != expected:
@@ -239,7 +246,7 @@ class LearnedOptionActor(nn.Module):
         m = self.manager_hidden_size
         manager = (h[..., :m].contiguous(), c[..., :m].contiguous())
         shape = (1, batch_size * self.num_options, self.option_recurrent_size)
-        return manager, (h[..., m:].reshape(shape).contiguous(), c[..., m:].reshape(shape).contiguous())
+        return UnpackedState((manager, (h[..., m:].reshape(shape).contiguous(), c[..., m:].reshape(shape).contiguous())))
 
     def _pack_state(self, manager_state, option_state, batch_size: int):
         shape = (1, batch_size, self.num_options * self.option_recurrent_size)

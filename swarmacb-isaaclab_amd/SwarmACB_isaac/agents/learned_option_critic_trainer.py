@@ -552,11 +552,13 @@ class LearnedOptionCriticTrainer(TrainerBase):
         # once over both streams' rows, the recurrences per stream
         next_h = batch["next_memory_h"].reshape(B * L, -1).unsqueeze(0).detach()
         next_c = batch["next_memory_c"].reshape(B * L, -1).unsqueeze(0).detach()
+        # the chunk-start memories split once into manager and option parts for the actor and its
+        # frozen copy (same sizes)
+        mem0 = self.actor._unpack_state(mem0, B)
         (a_item, a_ctx), (n_item, n_ctx) = self.actor.manager_stages(
             [(obs, mem0), (next_obs.reshape(B * L, 1, self.obs_dim), (next_h, next_c))])
         with torch.no_grad():
-            r_item, r_ctx = reference_actor.manager_stage(obs, (batch["memory_h"].unsqueeze(0),
-                                                                batch["memory_c"].unsqueeze(0)))
+            r_item, r_ctx = reference_actor.manager_stage(obs, mem0)
         outs = lstm_sequences([a_item, r_item + (True,), n_item])
         (a_item, a_ctx), (n_item, n_ctx) = self.actor.option_stages([a_ctx, n_ctx], [outs[0], outs[2]])
         with torch.no_grad():
