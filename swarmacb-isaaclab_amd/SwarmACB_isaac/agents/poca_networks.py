@@ -1176,10 +1176,12 @@ class POCACritic(nn.Module):
                 sets.append(self.obs_act_entity_enc(torch.cat([all_states, all_actions], dim=-1)))
             else:
                 sets.append(self._focal_entities(all_states, all_actions, focal_agent_ids))
-        ents = torch.cat(sets, dim=0)
+        # one pass: its tensors as they are (torch.cat of a single tensor is a copy launch)
+        ents = torch.cat(sets, dim=0) if len(sets) > 1 else sets[0]
         memory = None
         if self.lstm is not None:
-            memory = tuple(torch.cat([memories[name][i] for name in passes], dim=1) for i in (0, 1))
+            memory = tuple(torch.cat([memories[name][i] for name in passes], dim=1) if len(passes) > 1
+                           else memories[passes[0]][i] for i in (0, 1))
         pooled = self.self_attn(ents)
         encoding, item = self._tail_begin(pooled, memory, sequence_length)
         return item, (encoding, N, B)
