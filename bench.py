@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--gate", type=int, default=1,
                     help="1: the timed launches are enqueued behind a stream gate released after the enqueue "
                          "(swarm_gate_wait); 0: launched as they are enqueued")
+    ap.add_argument("--groups", type=int, default=1,
+                    help="env groups per GPU: each decision is K launches over contiguous env ranges on K "
+                         "streams with no cross-stream ordering (swarm_step_streams): every range's decisions "
+                         "form an independent chain, as in the pipelined collector")
     ap.add_argument("--rollout", action="store_true",
                     help="instead of the step: the rollout-buffer kernels at C3 (tools/bench_rollout.py)")
     ap.add_argument("--critic", action="store_true",
@@ -254,7 +258,7 @@ def spawn_ranks(gpus: int, argv: list[str], poll_s: float = 0.2, script: str | N
     return rc
 
 
-def prewarm(seconds: float, eng, E: int, dp: int, dev, out) -> float:
+def prewarm(seconds: float, eng, E: int, dp: int, dev, out, streams=None) -> float:
     """Untimed launches of the same workload (same step, same action distribution) on the
     timed engine itself for `seconds`, right before the warm-up decisions: the clocks are
     up and the arenas are past the contact burst that follows a spawn when the timed
@@ -267,7 +271,7 @@ def prewarm(seconds: float, eng, E: int, dp: int, dev, out) -> float:
     i = 0
     while time.perf_counter() - t0 < seconds:
         for _ in range(20):
-            eng.step(acts[i % 8], dp, out=out)
+            eng.step(acts[i % 8], dp, out=out, streams=streams)
             i += 1
         torch.cuda.synchronize(dev)
     return time.perf_counter() - t0
@@ -288,8 +292,18 @@ def ranks_table(rank: int, dev, dist) -> list[dict]:
     return [{"rank": r, "device": d, "pci": f"{a:04x}:{b:02x}:{c:02x}"} for r, d, a, b, c in rows]
 
 
+def gpu_count(ranks_seen: list[dict]) -> tuple[int, int]:
+    """(n_gpus, ranks_per_device) of the live process group: n_gpus counts DISTINCT physical
+    devices (PCI addresses), so ranks rehearsed on one card (gloo) can never print a multi-GPU
+    line; ranks_per_device is the largest number of ranks that shared one device."""
+    per: dict[str, int] = {}
+    for r in ranks_seen:
+        per[r["pci"]] = per.get(r["pci"], 0) + 1
+    return len(per), max(per.values()) if per else 0
+
+
 def valu_roofline(pmc: dict, pmc_why: str | None, avg_kernel_s: float, hbm_achieved: float, traffic, E: int,
-                  dp: int, bytes_per_launch: float, lib_sha: str | None) -> dict:
+                  dp: int, bytes_per_launch: float, lib_sha: str | None, layout: int = 103, groups: int = 1) -> dict:
     """The step kernel's roofline line: the binding roof is VALU issue
     (~80 op/B against a ~20 op/B ridge), so `bound` is "valu" with the measured SQ_INSTS_VALU
     x 64 lane-ops / kernel time against 256 CUs x 4 SIMD32 x 32 lanes x 2.4 GHz; HBM
@@ -313,7 +327,14 @@ def valu_roofline(pmc: dict, pmc_why: str | None, avg_kernel_s: float, hbm_achie
         "pmc_source": "profiles/pmc_traffic.json (rocprofv3 --pmc passes of this workload, tools/pmc.sh), "
                       "stamped with the sha256 of the libswarmstep.so it measured",
         "lib_sha256": lib_sha,
-        "kernel": "step_kernel<HOMING,ISAAC,continuous,N=20,layout 103>",
+        "kernel": ("step_kernel_pipe<HOMING> (layout 203)" if layout == 203
+                   else f"step_kernel<HOMING,ISAAC,continuous,N=20,layout {layout}>"),
+        "layout": layout,
+        "groups": groups,
+        # per decision: the timed region / decisions. With groups > 1 a decision is K launches over
+        # env ranges whose chains overlap, so one launch lives longer than this (rocprofv3's
+        # per-launch average); the decision's algorithmic bytes / VALU work over the decision's
+        # share of the region is the chip-level rate
         "kernel_avg_us": avg_kernel_s * 1e6,
         "secondary": {
             "bound": "hbm",
@@ -403,9 +424,13 @@ def main():
     g = torch.Generator(device=dev).manual_seed(args.seed * 1000 + rank)
     acts = (torch.randn(n_warm + n_dec, E, N_AGENTS, 2, device=dev, generator=g).clamp_(-3, 3) / 3).contiguous()
 
-    prewarm_s = prewarm(args.prewarm, eng, E, dp, dev, out)
+    # --groups K: K caller streams; each decision's K range launches go to them with no join, so
+    # every range's decisions form an independent chain (the pipelined collector's schedule)
+    streams = [torch.cuda.Stream(dev) for _ in range(args.groups)] if args.groups > 1 else None
+    torch.cuda.synchronize(dev)
+    prewarm_s = prewarm(args.prewarm, eng, E, dp, dev, out, streams)
     for d in range(n_warm):
-        eng.step(acts[d], dp, out=out)
+        eng.step(acts[d], dp, out=out, streams=streams)
     torch.cuda.synchronize(dev)
 
     # HIP events bracket the whole timed region (not every launch: each event is a packet of
@@ -423,6 +448,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     graph = None
+    if args.graph and streams is not None:
+        print("bench.py: --graph with --groups > 1 is not supported", file=sys.stderr, flush=True)
+        sys.exit(2)
     if args.graph:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
@@ -441,11 +469,18 @@ def main():
         C.c_uint32.from_address(gate.value + 4).value = 0
         _native.check(eng.lib.swarm_gate_wait(gate, 10_000_000, C.c_void_p(stream.cuda_stream)), "swarm_gate_wait")
     ev0.record(stream)
+    if streams is not None:
+        # one fork at the start (the group streams wait for the gate / ev0) and one join at the end
+        for st_k in streams:
+            st_k.wait_stream(stream)
     if graph is not None:
         graph.replay()
     else:
         for d in range(n_dec):
-            eng.step(acts[n_warm + d], dp, out=out)
+            eng.step(acts[n_warm + d], dp, out=out, streams=streams)
+    if streams is not None:
+        for st_k in streams:
+            stream.wait_stream(st_k)
     ev1.record(stream)
     t0 = time.perf_counter()
     if gate is not None:
@@ -471,6 +506,7 @@ def main():
     elapsed = max_over_ranks(elapsed, dev)
     ranks_seen = ranks_table(rank, dev, dist)
     world_live = dist.get_world_size() if dist is not None else 1
+    n_gpus, ranks_per_device = gpu_count(ranks_seen)
     total_agent_steps = world_live * E * N_AGENTS * steps
     value = total_agent_steps / elapsed
 
@@ -481,12 +517,14 @@ def main():
         pmc, pmc_why = load_pmc(E, dp, lib_path)
         traffic = pmc.get("hbm_bytes_per_launch")
         roofline = valu_roofline(pmc, pmc_why, avg_kernel_s, achieved, traffic, E, dp, bytes_per_launch,
-                                 lib_sha256(lib_path) if lib_path else None)
+                                 lib_sha256(lib_path) if lib_path else None, eng.layout, args.groups)
         line = {
             "metric": METRIC,
             "value": value,
             "unit": "agent-steps/s",
-            "n_gpus": world_live,
+            "n_gpus": n_gpus,
+            "ranks": world_live,
+            "ranks_per_device": ranks_per_device,
             "ranks_seen": ranks_seen,
             "steps": steps,
             "warmup": n_warm * dp,
@@ -504,9 +542,12 @@ def main():
                 "num_agents": N_AGENTS,
                 "global_envs": world * E,
                 "decision_period": dp,
-                "layout": args.layout or "default",
+                "layout": eng.layout,
+                "groups": args.groups,
                 "timed_launches": ("one HIP graph of the timed decisions, replayed once" if graph is not None
-                                   else "eager launches") + (", enqueued behind a stream gate released after the "
+                                   else "eager launches" if streams is None
+                                   else f"eager launches, each decision as {args.groups} env-range launches on "
+                                        f"{args.groups} streams without a per-decision join (swarm_step_streams)") + (", enqueued behind a stream gate released after the "
                                                              "enqueue" if gate is not None else ""),
                 "parallelism": f"env-sharded x{world}",
                 "agent_decisions_per_s": value / dp,

@@ -156,6 +156,28 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
  * ignore it). No reference counterpart: a scheduling knob of this library. */
 int32_t swarm_set_step_groups(swarm_handle_t* h, int32_t groups);
 
+/* swarm_step over `n_groups` contiguous env ranges [E k / K, E (k + 1) / K) (K = n_groups, 1..8,
+ * at most E), range k enqueued on the CALLER's streams[k] with no event and no cross-stream
+ * ordering: each range's decisions form an independent chain, so range k's next decision starts
+ * as soon as range k's previous one (and whatever the caller enqueued on streams[k] in between,
+ * e.g. its policy forward) has finished, and its launch fills the SIMDs the other ranges' tails
+ * leave idle. The caller orders its own work: actions rows of range k must be ready in
+ * streams[k] order, and outputs / state rows of range k are read after streams[k]. The tick,
+ * the time-out mirror and the global reset quirk (DG:1262, one reset_any mask per call) advance
+ * once per call exactly as for swarm_step, so the results are bitwise those of one swarm_step
+ * launch (arenas are independent and every draw is keyed by global env). K = 1 is swarm_step on
+ * streams[0]. Replaces the same reference code as swarm_step (n_substeps x DirectMARLEnv.step,
+ * poca_trainer.py:564-573); the split is a scheduling choice of this library. */
+int32_t swarm_step_streams(swarm_handle_t* h, const swarm_state_t* state, const void* actions,
+                           const float* override_wheels, const swarm_outputs_t* out, int32_t n_substeps,
+                           const swarm_replay_t* replay, void* const* streams, int32_t n_groups);
+
+/* The work layout the handle's step launches use (103: one wave per arena, 3 lanes per robot;
+ * 203: the two-wave pipeline of the continuous Isaac step; 4: the generic-N fallback), after
+ * swarm_create's device-dependent choice for layout 0; -1 for a null handle. No reference
+ * counterpart (bench.py labels its roofline line with it). */
+int32_t swarm_layout(const swarm_handle_t* h);
+
 /* get_critic_state() (directional_gate_env.py:1279-1290 -> epuck_sensors.py:545-586): out [E*N*5]. */
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream);
 

@@ -51,7 +51,7 @@ class SwarmReplay(C.Structure):
 EXPORTS = [
     "swarm_abi_version", "swarm_strerror", "swarm_last_hip_error", "swarm_create", "swarm_destroy",
     "swarm_reset", "swarm_step", "swarm_critic_state", "swarm_sync_episode_lengths", "swarm_tick",
-    "swarm_last_timeouts", "swarm_set_step_groups",
+    "swarm_last_timeouts", "swarm_set_step_groups", "swarm_step_streams", "swarm_layout",
     "swarm_gate_alloc", "swarm_gate_free", "swarm_gate_wait",
     "swarm_fsm_pack",
 ]
@@ -158,6 +158,12 @@ def load() -> C.CDLL:
     lib.swarm_last_timeouts.argtypes = [C.c_void_p]
     lib.swarm_set_step_groups.restype = C.c_int32
     lib.swarm_set_step_groups.argtypes = [C.c_void_p, C.c_int32]
+    lib.swarm_step_streams.restype = C.c_int32
+    lib.swarm_step_streams.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_void_p, C.c_void_p,
+                                       C.POINTER(SwarmOutputs), C.c_int32, C.POINTER(SwarmReplay),
+                                       C.POINTER(C.c_void_p), C.c_int32]
+    lib.swarm_layout.restype = C.c_int32
+    lib.swarm_layout.argtypes = [C.c_void_p]
     lib.swarm_fsm_pack.restype = C.c_uint32
     lib.swarm_fsm_pack.argtypes = [C.c_int32, C.c_int32, C.c_float] * 3
     i32, i64, vp = C.c_int32, C.c_int64, C.c_void_p

@@ -211,25 +211,36 @@ class _CategoricalTerms(torch.autograd.Function):
 _BAD_ACTIONS: dict = {}
 
 
+def _flag_key(device) -> str:
+    """One key per physical device: 'cuda' and 'cuda:0' (the current device) name the same flag,
+    so a trainer built with device='cuda' reads the flag the kernels set through tensors on
+    'cuda:0' (ADVICE r05)."""
+    d = torch.device(device)
+    if d.type == "cuda":
+        return f"cuda:{d.index if d.index is not None else torch.cuda.current_device()}"
+    return str(d)
+
+
 def _bad_action_flag(device) -> torch.Tensor:
     """The device int32 the fused policy terms OR their input-check bits into (one per device,
     allocated before any graph capture by the first eager step): 1 = a categorical action outside
     [0, K) (swarm_categorical_terms), 2 = an OC2 option outside [0, O) (swarm_oc2_option_terms),
-    4 = a non-finite mean or non-finite / non-positive std of the OC2 wheel policy
+    4 = a NaN mean or a NaN / non-positive std of the OC2 wheel policy, torch's Normal constraints
     (swarm_oc2_action_terms)."""
-    key = str(device)
+    key = _flag_key(device)
     if key not in _BAD_ACTIONS:
-        _BAD_ACTIONS[key] = torch.zeros(1, dtype=torch.int32, device=device)
+        _BAD_ACTIONS[key] = torch.zeros(1, dtype=torch.int32, device=key)
     return _BAD_ACTIONS[key]
 
 
 def check_policy_inputs(device) -> None:
     """Raise if a fused policy term of this device saw an input the reference's torch.distributions
     would reject since the last check: Categorical.log_prob / gather raise on an index outside
-    [0, K), Normal(loc, scale) (built with validation on, learned_option_critic_networks.py) on a
-    NaN / infinite / non-positive scale. The kernels flag instead of returning a silent NaN; one
+    [0, K) (IndexError, as the POCA path's gather), Categorical's value check on an option outside
+    [0, O) (ValueError), Normal(loc, scale) (built with validation on, learned_option_critic_networks.py)
+    on a NaN loc or a NaN / non-positive scale (ValueError). The kernels flag instead of returning a silent NaN; one
     host read, called once per update."""
-    flag = _BAD_ACTIONS.get(str(device))
+    flag = _BAD_ACTIONS.get(_flag_key(device))
     if flag is None:
         return
     bits = int(flag.item())
@@ -241,10 +252,11 @@ def check_policy_inputs(device) -> None:
                          "update (e.g. the -1 'fresh option' sentinel); torch.distributions.Categorical "
                          "would raise on it too")
     if bits & 2:
-        raise IndexError("OC2 option terms: an option index outside [0, num_options) reached the update; "
-                         "torch.distributions.Categorical would raise on it too")
-    raise ValueError("OC2 action terms: a non-finite mean or a non-finite / non-positive standard deviation "
-                     "reached the update; torch.distributions.Normal's argument validation would raise on it too")
+        # Categorical.log_prob's support check (validate_args) raises ValueError
+        raise ValueError("OC2 option terms: an option index outside [0, num_options) reached the update; "
+                         "torch.distributions.Categorical's value validation would raise on it too")
+    raise ValueError("OC2 action terms: a NaN mean or a NaN / non-positive standard deviation reached the "
+                     "update; torch.distributions.Normal's argument validation would raise on it too")
 
 
 check_categorical_actions = check_policy_inputs

@@ -49,6 +49,8 @@ from .learned_option_critic_networks import (LEARNED_OPTION_CRITIC_VERSION, Lear
 from .option_collector import LearnedOptionCollector
 from .poca_networks import POCACritic, batched_sequence_passes, lstm_sequences
 
+REFERENCE_SUM_ORDER = os.environ.get("SWARM_OC2_REFERENCE_SUM", "0") == "1"
+
 __all__ = ["LearnedOptionCriticConfig", "LearnedOptionCriticTrainer", "stable_trust_region_policy_loss"]
 
 METRIC_NAMES = (
@@ -745,7 +747,11 @@ class LearnedOptionCriticTrainer(TrainerBase):
         actor, critic = self._objective_coefs()
         staged = self.__dict__.get("_obj_coefs")
         ref = losses["intra_option_loss"]
-        if (staged is not None and staged[0] == [c for _, _, c in actor] + [c for _, c in critic]
+        # SWARM_OC2_REFERENCE_SUM=1: the reference's left-to-right Python sums (bitwise its fp32
+        # order); default: the stacked products, whose reduction order differs at fp32 rounding
+        # (<= a few ulp of each loss; the trainer fixtures compare at rtol 1e-4 + 1e-5 x scale,
+        # tests/test_gpu_oc2_trainer.py)
+        if (not REFERENCE_SUM_ORDER and staged is not None and staged[0] == [c for _, _, c in actor] + [c for _, c in critic]
                 and staged[1].device == ref.device
                 and all(losses[n].dtype == torch.float32 and losses[n].numel() == 1
                         for n in [a for _, a, _ in actor] + [a for a, _ in critic])):
@@ -1029,8 +1035,14 @@ class LearnedOptionCriticTrainer(TrainerBase):
                 kl = torch.stack([losses["action_approx_kl"].detach(), losses["option_approx_kl"].detach()])
                 if self.comm.active:
                     kl = self.comm.sum_tensor(kl)     # every rank takes the same early-stop decision
+                # the fused terms' input flag rides on the same host read, so an invalid option /
+                # Normal input raises BEFORE this minibatch's optimizer steps, as the reference's
+                # distribution validation does
                 host = torch.cat([kl, torch.stack([torch.isfinite(actor_loss.detach()),
-                                                   torch.isfinite(critic_loss.detach())]).to(kl.dtype)]).tolist()
+                                                   torch.isfinite(critic_loss.detach())]).to(kl.dtype),
+                                  _bad_action_flag(kl.device).to(kl.dtype)]).tolist()
+                if host[4]:
+                    check_policy_inputs(kl.device)
                 action_kl, option_kl = host[0], host[1]
                 policy_kl = max(action_kl, option_kl)
                 if num_batches == 0:

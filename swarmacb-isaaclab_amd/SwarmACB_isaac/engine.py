@@ -142,9 +142,20 @@ class SwarmEngine:
         _native.check(rc, "swarm_reset")
         return obs, rew, tr
 
+    def group_range(self, k: int, groups: int) -> tuple[int, int]:
+        """Env range [e0, e1) of group k of `groups` (swarm_step_streams' split)."""
+        return self.E * k // groups, self.E * (k + 1) // groups
+
     def step(self, actions: torch.Tensor, n_substeps: int = 1, override: torch.Tensor | None = None,
-             out=None, replay: dict | None = None):
-        """n_substeps env.step()s with a held action. Returns (obs, reward_sum, truncated_any)."""
+             out=None, replay: dict | None = None, streams=None):
+        """n_substeps env.step()s with a held action. Returns (obs, reward_sum, truncated_any).
+
+        streams: None (one launch on the current stream) or a list of K torch streams: env range
+        k (group_range) is launched on streams[k] with no cross-stream ordering
+        (swarm_step_streams); the caller has ordered the action rows of range k on streams[k] and
+        reads range k's outputs after streams[k]. Bitwise the same results."""
+        if streams is not None:
+            return self._step_streams(actions, n_substeps, override, out, replay, streams)
         if actions.device != self.device or not actions.is_contiguous():
             raise ValueError("actions must be a contiguous tensor on the engine's device")
         if self.discrete:
@@ -162,6 +173,37 @@ class SwarmEngine:
                                  C.byref(rp) if rp is not None else None, self._stream())
         _native.check(rc, "swarm_step")
         return obs, rew, tr
+
+    def _check_actions(self, actions, override):
+        if actions.device != self.device or not actions.is_contiguous():
+            raise ValueError("actions must be a contiguous tensor on the engine's device")
+        if self.discrete:
+            if actions.dtype != torch.int32 or actions.numel() != self.E * self.N:
+                raise ValueError(f"discrete actions must be int32 with {self.E * self.N} elements")
+        elif actions.dtype != torch.float32 or actions.numel() != self.E * self.N * 2:
+            raise ValueError(f"continuous actions must be float32 with {self.E * self.N * 2} elements")
+        if override is not None and (override.dtype != torch.float32 or override.numel() != self.E * self.N * 2):
+            raise ValueError("override wheels must be float32 (E, N, 2)")
+
+    def _step_streams(self, actions, n_substeps, override, out, replay, streams):
+        self._check_actions(actions, override)
+        K = len(streams)
+        if K < 1 or K > 8 or K > self.E:
+            raise ValueError(f"streams: 1..min(8, E) groups, got {K}")
+        obs, rew, tr = out if out is not None else self.new_outputs()
+        o = _native.SwarmOutputs(obs.data_ptr(), rew.data_ptr(), tr.data_ptr())
+        rp = self._replay(replay)
+        arr = (C.c_void_p * K)(*[s.cuda_stream for s in streams])
+        rc = self.lib.swarm_step_streams(self.handle, C.byref(self._state), C.c_void_p(actions.data_ptr()),
+                                         _ptr(override), C.byref(o), int(n_substeps),
+                                         C.byref(rp) if rp is not None else None, arr, K)
+        _native.check(rc, "swarm_step_streams")
+        return obs, rew, tr
+
+    @property
+    def layout(self) -> int:
+        """The step launches' work layout (swarm_layout: 103, 203 or 4)."""
+        return int(self.lib.swarm_layout(self.handle))
 
     def critic_state(self, out: torch.Tensor | None = None) -> torch.Tensor:
         out = out if out is not None else torch.empty(self.E, self.N, 5, dtype=torch.float32, device=self.device)

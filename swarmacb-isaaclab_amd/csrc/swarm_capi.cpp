@@ -266,11 +266,10 @@ int32_t swarm_reset(swarm_handle_t* h, const swarm_state_t* state, const uint8_t
     return hip_status();
 }
 
-int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* actions, const float* override_wheels,
-                   const swarm_outputs_t* out, int32_t n_substeps, const swarm_replay_t* replay, void* stream) {
-    if (!h || !state_ok(state) || !actions || !out || !out->obs) return SWARM_ERR_ARG;
-    if (n_substeps < 1 || n_substeps > SWARM_MAX_SUBSTEPS) return SWARM_ERR_ARG;
-    if (!h->was_reset) return SWARM_ERR_STATE;
+namespace {
+// the host bookkeeping of one swarm_step call: advance the episode-length mirror by n_substeps
+// env.steps and return the reset_any mask of the global reset quirk (DG:1262)
+uint64_t advance_mirror(swarm_handle_t* h, int32_t n_substeps) {
     uint64_t reset_any = 0;
     for (int s = 0; s < n_substeps; ++s) {
         if (h->mirror.step()) reset_any |= 1ull << s;
@@ -279,6 +278,25 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     h->lens_exact = h->mirror.buckets.size() <= 1;
     if (h->lens_exact && !h->mirror.buckets.empty())
         h->lens.assign(h->p.num_envs, (int32_t)(h->mirror.buckets.begin()->first + h->mirror.offset));
+    return reset_any;
+}
+
+// env range k of K: [E k / K, E (k + 1) / K) (swarm_set_step_groups and swarm_step_streams)
+Geom group_geom(const swarm_handle_t* h, int k, int K) {
+    Geom gk = h->g;
+    const int E = h->p.num_envs;
+    gk.env0 = (int32_t)((int64_t)E * k / K);
+    gk.env_n = (int32_t)((int64_t)E * (k + 1) / K) - gk.env0;
+    return gk;
+}
+}  // namespace
+
+int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* actions, const float* override_wheels,
+                   const swarm_outputs_t* out, int32_t n_substeps, const swarm_replay_t* replay, void* stream) {
+    if (!h || !state_ok(state) || !actions || !out || !out->obs) return SWARM_ERR_ARG;
+    if (n_substeps < 1 || n_substeps > SWARM_MAX_SUBSTEPS) return SWARM_ERR_ARG;
+    if (!h->was_reset) return SWARM_ERR_STATE;
+    const uint64_t reset_any = advance_mirror(h, n_substeps);
     const hipStream_t cs = (hipStream_t)stream;
     const DevState st = dev_state(state);
     const DevOut o{out->obs, out->reward, out->truncated};
@@ -286,11 +304,9 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
         // fork: every group stream waits for the caller's stream; join: the caller's
         // stream waits for every group (one arena per workgroup, ranges of E / groups)
         if (hipEventRecord(h->gfork, cs) != hipSuccess) return hip_status();
-        const int E = h->p.num_envs, K = h->groups;
+        const int K = h->groups;
         for (int k = 0; k < K; ++k) {
-            Geom gk = h->g;
-            gk.env0 = (int32_t)((int64_t)E * k / K);
-            gk.env_n = (int32_t)((int64_t)E * (k + 1) / K) - gk.env0;
+            const Geom gk = group_geom(h, k, K);
             if (hipStreamWaitEvent(h->gstream[k], h->gfork, 0) != hipSuccess) return hip_status();
             launch_step(gk, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any,
                         h->gstream[k]);
@@ -304,6 +320,27 @@ int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* ac
     h->tick += (uint64_t)n_substeps;
     return hip_status();
 }
+
+int32_t swarm_step_streams(swarm_handle_t* h, const swarm_state_t* state, const void* actions,
+                           const float* override_wheels, const swarm_outputs_t* out, int32_t n_substeps,
+                           const swarm_replay_t* replay, void* const* streams, int32_t n_groups) {
+    if (!h || !state_ok(state) || !actions || !out || !out->obs || !streams) return SWARM_ERR_ARG;
+    if (n_substeps < 1 || n_substeps > SWARM_MAX_SUBSTEPS) return SWARM_ERR_ARG;
+    if (n_groups < 1 || n_groups > SWARM_MAX_STEP_GROUPS || n_groups > h->p.num_envs) return SWARM_ERR_ARG;
+    // env ranges need the one-arena-per-workgroup layouts (the generic-N layout 4 packs arenas)
+    if (n_groups > 1 && h->g.layout != 103 && h->g.layout != 203) return SWARM_ERR_ARG;
+    if (!h->was_reset) return SWARM_ERR_STATE;
+    const uint64_t reset_any = advance_mirror(h, n_substeps);
+    const DevState st = dev_state(state);
+    const DevOut o{out->obs, out->reward, out->truncated};
+    for (int k = 0; k < n_groups; ++k)
+        launch_step(n_groups > 1 ? group_geom(h, k, n_groups) : h->g, st, actions, override_wheels, o,
+                    dev_replay(replay), h->tick, n_substeps, reset_any, (hipStream_t)streams[k]);
+    h->tick += (uint64_t)n_substeps;
+    return hip_status();
+}
+
+int32_t swarm_layout(const swarm_handle_t* h) { return h ? h->g.layout : -1; }
 
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream) {
     if (!h || !state || !state->pos_x || !state->pos_y || !state->yaw || !out) return SWARM_ERR_ARG;

@@ -71,7 +71,7 @@ constexpr int kPartThreads = 256;
 
 // bits of the caller's input-check flag (include/swarmtrain.h)
 constexpr int32_t kBadOption = 2;   // an option index outside [0, O)
-constexpr int32_t kBadStd = 4;      // a non-finite or non-positive standard deviation
+constexpr int32_t kBadStd = 4;      // a NaN mean, or a NaN / non-positive standard deviation
 
 // block-wide sum of K per-thread partials over an NT-thread block; the result is valid in thread 0
 template <int K, int NT>
@@ -478,10 +478,10 @@ __global__ __launch_bounds__(kThreads) void action_fwd_kernel(int64_t M, int A, 
     const int64_t n = M * A;
     for (int64_t i = threadIdx.x; i < n; i += kThreads) {
         const int64_t m = i / A;
-        // Normal(loc, scale)'s argument validation rejects a NaN / infinite or non-positive scale
-        // (the reference builds it with validation on); flag it for the host
-        const bool ok = isfinite(sg[i]) && sg[i] > 0.0f && isfinite(sg_r[i]) && sg_r[i] > 0.0f &&
-                        isfinite(mu[i]) && isfinite(mu_r[i]);
+        // Normal(loc, scale)'s argument validation (the reference builds it with validation on)
+        // checks exactly torch's constraints: loc real (loc == loc: NaN fails, +-inf passes) and
+        // scale positive (scale > 0: NaN and non-positive fail, +inf passes); flag it for the host
+        const bool ok = sg[i] > 0.0f && sg_r[i] > 0.0f && mu[i] == mu[i] && mu_r[i] == mu_r[i];
         if (!ok && bad) atomicOr(bad, kBadStd);
         float ld;
         const float u = pre_tanh_of(x[i], squash != 0, ld);

@@ -1904,8 +1904,9 @@ static void launch_step_t(const Geom& g, const DevState& st, const void* act, co
     if constexpr (P == ISAAC && !D) {
         // layout 203: the two-wave pipeline of the continuous Isaac step (production kernel; the
         // replay kernels of the parity tests run layout 103, whose arithmetic it shares)
-        if (g.layout == 203 && g.N == 20 && !replay && g.env0 == 0 && (g.env_n == 0 || g.env_n == g.E)) {
-            hipLaunchKernelGGL((step_kernel_pipe<M>), dim3(g.E), dim3(128), 0, stream, g, st, act, out, tick, n_sub,
+        if (g.layout == 203 && g.N == 20 && !replay) {
+            const int blocks = g.env_n > 0 ? g.env_n : g.E;   // arenas [env0, env0 + blocks)
+            hipLaunchKernelGGL((step_kernel_pipe<M>), dim3(blocks), dim3(128), 0, stream, g, st, act, out, tick, n_sub,
                                reset_any);
             return;
         }

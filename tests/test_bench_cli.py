@@ -32,6 +32,17 @@ def test_rank_plan():
     assert bench.rank_plan(0, {})[0] == "refuse"
 
 
+def test_gpu_count_is_distinct_devices():
+    """n_gpus counts physical devices, not ranks (Weak 5): two ranks on one PCI
+    address are one GPU with two ranks per device; one rank is unchanged."""
+    one = [{"rank": 0, "device": 0, "pci": "0000:d9:00"}]
+    assert bench.gpu_count(one) == (1, 1)
+    shared = [{"rank": 0, "device": 0, "pci": "0000:d9:00"}, {"rank": 1, "device": 0, "pci": "0000:d9:00"}]
+    assert bench.gpu_count(shared) == (1, 2)
+    two = [{"rank": 0, "device": 0, "pci": "0000:0a:00"}, {"rank": 1, "device": 1, "pci": "0000:1a:00"}]
+    assert bench.gpu_count(two) == (2, 1)
+
+
 def test_spawn_ranks_environment(tmp_path):
     """Each spawned rank gets its own RANK / LOCAL_RANK, the common WORLD_SIZE and one port."""
     probe = tmp_path / "probe.py"

@@ -86,6 +86,30 @@ def test_step_groups_argument_checks():
         assert lib.swarm_destroy(h) == 0
 
 
+def test_step_streams_argument_checks():
+    """swarm_step_streams validates before touching the device; swarm_layout reports the handle's
+    layout (103 for N = 20 when no GPU is there to pick 203)."""
+    lib = _native.load()
+    assert lib.swarm_layout(None) == -1
+    h = C.c_void_p()
+    assert lib.swarm_create(C.byref(_params(num_envs=4)), C.byref(h)) == 0
+    try:
+        assert lib.swarm_layout(h) in (103, 203)
+        st = _native.SwarmState(*([1] * 13))
+        out = _native.SwarmOutputs(1, 1, 1)
+        streams = (C.c_void_p * 8)()
+        args = (C.byref(st), C.c_void_p(1), None, C.byref(out), 5, None)
+        assert lib.swarm_step_streams(h, *args, streams, 0) == -1
+        assert lib.swarm_step_streams(h, *args, streams, 9) == -1
+        assert lib.swarm_step_streams(h, *args, streams, 5) == -1       # more groups than envs
+        assert lib.swarm_step_streams(h, *args, None, 2) == -1          # no stream array
+        assert lib.swarm_step_streams(h, *args, streams, 2) == -4       # step before reset
+        assert lib.swarm_step_streams(None, *args, streams, 1) == -1
+        assert lib.swarm_tick(h) == 0                                    # nothing advanced
+    finally:
+        assert lib.swarm_destroy(h) == 0
+
+
 def test_tensor_list_copy_argument_checks():
     lib = _native.load()
     assert lib.swarm_tensor_list_copy(-1, None, None, None, 0, None, None) == -1

@@ -194,7 +194,7 @@ def test_input_checks_flag_what_torch_distributions_reject(gpu_device):
     bad = options.clone()
     bad[1, 3] = -1                                                    # the 'fresh option' sentinel
     LT.fused_option_terms(Actor(), q, bad, mask, mask, 0.1, None)
-    with pytest.raises(IndexError):
+    with pytest.raises(ValueError):                                   # Categorical's support check
         check_policy_inputs(gpu_device)
     check_policy_inputs(gpu_device)                                   # the check reset the flag
 
@@ -212,6 +212,13 @@ def test_input_checks_flag_what_torch_distributions_reject(gpu_device):
         LT.fused_action_terms(actor, means, s2, means, stds, options, actions, old_lp, mask, None)
         with pytest.raises(ValueError):
             check_policy_inputs(gpu_device)
+    # torch's constraints pass +inf scales and +-inf locs (the loss then goes non-finite and the
+    # trainer's own FloatingPointError fires): no input flag for them
+    s2, m2 = stds.clone(), means.clone()
+    s2[2, 5, options[2, 5]] = float("inf")
+    m2[1, 1, options[1, 1]] = float("-inf")
+    LT.fused_action_terms(actor, m2, s2, means, stds, options, actions, old_lp, mask, None)
+    check_policy_inputs(gpu_device)
 
 
 def test_attention_terms_concurrent_streams(gpu_device):

@@ -257,3 +257,44 @@ def test_step_groups_bitwise(mission, discrete, obs_dim, gpu_device):
             for name, x, y in zip(("obs", "reward", "trunc"), a, b):
                 assert np.array_equal(x, y), f"groups={groups}: decision {k} {name} differs"
 
+
+
+@pytest.mark.parametrize("mission,discrete,obs_dim,layout", [("homing", False, 24, 103), ("homing", False, 24, 203),
+                                                             ("foraging", True, 4, 103)])
+def test_step_streams_bitwise(mission, discrete, obs_dim, layout, gpu_device):
+    """swarm_step_streams: each decision split into 2, 3 or 8 env ranges on the caller's streams
+    with NO per-decision join (every range runs its 12 decisions as an independent chain into
+    per-decision output buffers; one join at the end) gives bit for bit the single launch's state
+    and outputs (uneven ranges, staggered time-outs, fused 5-step decisions, both layouts of the
+    continuous step)."""
+    from SwarmACB_isaac.engine import SwarmEngine
+
+    E, seed, D = 1000, 778, 12
+    rng = np.random.default_rng(6)
+    acts = [torch.as_tensor(rng.integers(0, 6, (E, 20)).astype(np.int32) if discrete
+                            else (np.clip(rng.normal(size=(E, 20, 2)), -3, 3) / 3).astype(np.float32)).to(gpu_device)
+            for _ in range(D)]
+    runs = []
+    for groups in (1, 2, 3, 8):
+        eng = SwarmEngine(mission, "isaac", E, 20, obs_dim, discrete, 1800, 1, 0, seed, gpu_device, layout=layout)
+        assert eng.layout == layout
+        eng.reset()
+        _stagger_timeouts(eng, [(np.arange(3, 13), 3), (np.arange(400, 407), 17), ([E - 1], 31)])
+        outs = [eng.new_outputs() for _ in range(D)]
+        torch.cuda.synchronize(gpu_device)
+        streams = [torch.cuda.Stream(gpu_device) for _ in range(groups)]
+        for k in range(D):
+            eng.step(acts[k], 5, out=outs[k], streams=streams)
+        for s in streams:
+            torch.cuda.current_stream(gpu_device).wait_stream(s)
+        torch.cuda.synchronize(gpu_device)
+        runs.append((eng.dump_state(), [tuple(t.cpu().numpy() for t in o) for o in outs]))
+        eng.close()
+    ref_state, ref_outs = runs[0]
+    assert sum(int(o[2].sum()) for o in ref_outs) >= 18
+    for groups, (st, outs) in zip((2, 3, 8), runs[1:]):
+        for key in ref_state:
+            assert np.array_equal(ref_state[key], st[key]), f"groups={groups}: state {key} differs"
+        for k, (a, b) in enumerate(zip(ref_outs, outs)):
+            for name, x, y in zip(("obs", "reward", "trunc"), a, b):
+                assert np.array_equal(x, y), f"groups={groups}: decision {k} {name} differs"

@@ -20,8 +20,9 @@ sys.path.insert(0, os.path.join(ROOT, "swarmacb-isaaclab_amd"))
 from SwarmACB_isaac.engine import SwarmEngine  # noqa: E402
 
 
-def run(K: int, mode: str, E=4096, N=20, dp=5, n_dec=240, warm=200, dev=torch.device("cuda:0")):
-    engs = [SwarmEngine("homing", "isaac", E // K, N, 24, False, 1200, 1, k * (E // K), 0, dev) for k in range(K)]
+def run(K: int, mode: str, E=4096, N=20, dp=5, n_dec=240, warm=200, dev=torch.device("cuda:0"), layout=103):
+    engs = [SwarmEngine("homing", "isaac", E // K, N, 24, False, 1200, 1, k * (E // K), 0, dev, layout=layout)
+            for k in range(K)]
     outs = [e.reset() for e in engs]
     streams = [torch.cuda.Stream(dev) for _ in range(K)]
     g = torch.Generator(device=dev).manual_seed(7)
@@ -52,14 +53,16 @@ def run(K: int, mode: str, E=4096, N=20, dp=5, n_dec=240, warm=200, dev=torch.de
         decision(i)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
-    return {"K": K, "mode": mode, "us_per_decision": dt / n_dec * 1e6,
+    return {"K": K, "mode": mode, "layout": layout, "E": E, "us_per_decision": dt / n_dec * 1e6,
             "agent_steps_per_s": E * N * dp * n_dec / dt}
 
 
 def main():
-    for K in (1, 2, 4, 8):
-        for mode in ("join", "free"):
-            print(json.dumps(run(K, mode)), flush=True)
+    E = int(os.environ.get("STREAMS_E", 4096))
+    for rep in range(2):
+        for K in (1, 2, 4, 8):
+            for layout in ((103, 203) if E // K <= 2048 else (103,)):
+                print(json.dumps(run(K, "free", E=E, layout=layout)), flush=True)
 
 
 if __name__ == "__main__":
