@@ -180,6 +180,10 @@ int32_t swarm_layout(const swarm_handle_t* h);
 
 /* get_critic_state() (directional_gate_env.py:1279-1290 -> epuck_sensors.py:545-586): out [E*N*5]. */
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream);
+/* The same for the env range [env0, env0 + env_n) only: out [env_n*N*5] (the pipelined collector's
+ * per-group critic state, agents/collector.py, on the group's stream). */
+int32_t swarm_critic_state_range(swarm_handle_t* h, const swarm_state_t* state, int32_t env0, int32_t env_n,
+                                 float* out, void* stream);
 
 /* Host mirror of episode_length_buf (used to evaluate the reference's global
  * "any env reset -> _resolve_collisions() on all envs" quirk, DG:1262, without

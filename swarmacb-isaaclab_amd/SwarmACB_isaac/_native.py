@@ -52,6 +52,7 @@ EXPORTS = [
     "swarm_abi_version", "swarm_strerror", "swarm_last_hip_error", "swarm_create", "swarm_destroy",
     "swarm_reset", "swarm_step", "swarm_critic_state", "swarm_sync_episode_lengths", "swarm_tick",
     "swarm_last_timeouts", "swarm_set_step_groups", "swarm_step_streams", "swarm_layout",
+    "swarm_critic_state_range",
     "swarm_gate_alloc", "swarm_gate_free", "swarm_gate_wait",
     "swarm_fsm_pack",
 ]
@@ -162,6 +163,9 @@ def load() -> C.CDLL:
     lib.swarm_step_streams.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_void_p, C.c_void_p,
                                        C.POINTER(SwarmOutputs), C.c_int32, C.POINTER(SwarmReplay),
                                        C.POINTER(C.c_void_p), C.c_int32]
+    lib.swarm_critic_state_range.restype = C.c_int32
+    lib.swarm_critic_state_range.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_int32, C.c_int32, C.c_void_p,
+                                             C.c_void_p]
     lib.swarm_layout.restype = C.c_int32
     lib.swarm_layout.argtypes = [C.c_void_p]
     lib.swarm_fsm_pack.restype = C.c_uint32

@@ -104,8 +104,21 @@ class POCARolloutCollector:
     first decision is taken on (env.reset()'s, stacked)."""
 
     def __init__(self, env, buffer, actor, critic, *, decision_period: int, reward_strength: float = 1.0,
-                 discrete: bool = False, num_actions: int = 0, recurrent: bool = False):
+                 discrete: bool = False, num_actions: int = 0, recurrent: bool = False, groups: int = 1):
         self.env, self.buffer, self.actor, self.critic = env, buffer, actor, critic
+        # groups > 1: the pipelined decision loop (collect's docstring); 1 = one stream
+        self.groups = int(groups)
+        if self.groups > 1:
+            engine = getattr(env, "engine", None)
+            if engine is None or discrete or recurrent:
+                raise ValueError("groups > 1 pipelines the continuous, non-recurrent (dandelion) decision loop "
+                                 "over a SwarmEngine env")
+            if self.groups > min(8, env.num_envs):
+                raise ValueError(f"groups must be 1..min(8, num_envs), got {self.groups}")
+            if engine.max_episode_length < 2 * int(decision_period):
+                raise ValueError("groups > 1 needs max_episode_length >= 2 x decision_period (an env times out "
+                                 "in at most one of two consecutive decisions)")
+            self._streams = [torch.cuda.Stream(env.device) for _ in range(self.groups)]
         self.decision_period = int(decision_period)
         self.reward_strength = float(reward_strength)
         self.discrete, self.num_actions, self.recurrent = discrete, num_actions, recurrent
@@ -148,6 +161,8 @@ class POCARolloutCollector:
         buf, E, N, dp = self.buffer, self.num_envs, self.num_agents, self.decision_period
         if reset_buffer:
             buf.reset()
+        if self.groups > 1:
+            return self._collect_pipelined(obs, int(rollout_steps))
         for _ in range(int(rollout_steps)):
             t = buf.ptr
             if t >= buf.horizon:
@@ -227,6 +242,9 @@ class POCARolloutCollector:
             buf.ptr = t + 1
             obs = obs_next
             self.global_step += E * N
+        return self._finish(obs)
+
+    def _finish(self, obs):
         last_state = self.env.get_critic_state()
         if self.recurrent:
             last_tv = self.critic.critic_pass(last_state, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
@@ -234,3 +252,72 @@ class POCARolloutCollector:
             last_tv = self.critic.critic_pass(last_state).squeeze(-1)
         buf.compute_returns_and_advantages(last_tv)
         return obs.clone()
+
+    def _collect_pipelined(self, obs: torch.Tensor, rollout_steps: int) -> torch.Tensor:
+        """The decision loop with the envs split into K contiguous groups, each an independent chain
+        on its own stream (the schedule `bench.py --groups K` times): per decision, group k's actor
+        forward, sample, critic state, critic value + baselines and buffer rows are enqueued on
+        stream k, then ONE swarm_step_streams call launches every group's decision on its stream.
+        Group k's next decision needs only its own observation rows, so it starts as soon as its
+        own step ends, while the other groups are still stepping: one group's launch tail overlaps
+        the others' work, and there is no per-decision join of the groups. The episode bookkeeping
+        (swarm_decision_record, in env order, with the completed-episode log) runs on the caller's
+        stream after the decision's group steps (it reads per-decision reward buffers, so no group
+        waits for it).
+
+        The same actions as the one-stream loop: Normal.sample() is torch.normal(loc, scale), i.e.
+        eps.normal_() over the (E*N, A) rows then eps * scale + loc; the rollout's eps are drawn
+        up front on the caller's stream in decision order (the same generator calls, in the same
+        order, as one sample() per decision), and each group applies its rows' scale and loc."""
+        buf, E, N, dp, K = self.buffer, self.num_envs, self.num_agents, self.decision_period, self.groups
+        eng, dev, A = self.env.engine, self.device, buf.act_dim
+        main = torch.cuda.current_stream(dev)
+        ranges = [eng.group_range(k, K) for k in range(K)]
+        t0 = buf.ptr
+        if t0 + rollout_steps > buf.horizon:
+            raise RuntimeError(buf._full_message)
+        eps = [torch.empty(E * N, A, device=dev).normal_() for _ in range(rollout_steps)]
+        rews = [torch.empty(E, device=dev) for _ in range(rollout_steps)]
+        truncs = [torch.empty(E, dtype=torch.uint8, device=dev) for _ in range(rollout_steps)]
+        env_act = torch.empty(E, N, A, device=dev)
+        if obs.data_ptr() != buf.obs[t0].data_ptr():
+            buf.obs[t0] = obs
+        for s in self._streams:            # one fork: the buffer row, eps and the env state are ready
+            s.wait_stream(main)
+        done_ev = [torch.cuda.Event() for _ in range(K)]
+        for i in range(rollout_steps):
+            t = t0 + i
+            flat_obs = buf.obs[t].reshape(E * N, -1)
+            for k, (e0, e1) in enumerate(ranges):
+                with torch.cuda.stream(self._streams[k]):
+                    r0, r1 = e0 * N, e1 * N
+                    dist = self.actor.get_dist(flat_obs[r0:r1])
+                    act = eps[i][r0:r1] * dist.scale + dist.loc          # torch.normal's mul_ then add_
+                    acts = act.view(e1 - e0, N, A)
+                    buf.log_probs[t][e0:e1] = dist.log_prob(act).view(e1 - e0, N, A)
+                    buf.actions[t][e0:e1] = acts
+                    cs = eng.critic_state_range(e0, e1, out=buf.critic_states[t][e0:e1])
+                    (team_val, _), (baselines, _) = self._value_and_baselines(cs, acts)
+                    buf.team_values[t][e0:e1] = team_val.squeeze(-1)
+                    buf.baselines[t][e0:e1] = baselines
+                    env_act[e0:e1] = acts.clamp(-3, 3) / 3
+            obs_out = buf.obs[t + 1] if t + 1 < buf.horizon else self._obs
+            eng.step(env_act, dp, out=(obs_out, rews[i], truncs[i]), streams=self._streams)
+            for k in range(K):
+                done_ev[k].record(self._streams[k])
+                main.wait_event(done_ev[k])
+            # the bookkeeping of decision i on the caller's stream (after every group's step i)
+            if eng.last_timeouts:
+                tv = self.critic.critic_pass(self.env.completed_terminal_critic_state).squeeze(-1)
+            else:
+                tv = self._zero_values
+            self.recorder.record(
+                {"rewards": buf.rewards[t], "dones": buf.dones[t], "timeouts": buf.timeouts[t],
+                 "timeout_values": buf.timeout_values[t]},
+                rews[i], truncs[i], self.env.completed_group_reward, dp, self.reward_strength,
+                timeout_value_raw=tv.contiguous())
+            buf.ptr = t + 1
+            self.global_step += E * N
+        for s in self._streams:            # one join before the returns (and before eps are freed)
+            main.wait_stream(s)
+        return self._finish(buf.obs[buf.ptr] if buf.ptr < buf.horizon else self._obs)

@@ -211,6 +211,17 @@ class SwarmEngine:
                                                   self._stream()), "swarm_critic_state")
         return out
 
+    def critic_state_range(self, e0: int, e1: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """critic_state() of the envs [e0, e1) only, on the current stream (swarm_critic_state_range)."""
+        n = int(e1) - int(e0)
+        out = out if out is not None else torch.empty(n, self.N, 5, dtype=torch.float32, device=self.device)
+        if out.numel() != n * self.N * 5 or not out.is_contiguous() or out.dtype != torch.float32:
+            raise ValueError("out must be a contiguous float32 (e1 - e0, N, 5) tensor")
+        _native.check(self.lib.swarm_critic_state_range(self.handle, C.byref(self._state), int(e0), n,
+                                                        C.c_void_p(out.data_ptr()), self._stream()),
+                      "swarm_critic_state_range")
+        return out
+
     def sync_episode_lengths(self):
         """Refresh the host mirror after episode lengths were written from the host."""
         lens = np.ascontiguousarray(self.episode_length.cpu().numpy().astype(np.int32))

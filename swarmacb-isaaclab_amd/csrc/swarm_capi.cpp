@@ -348,6 +348,17 @@ int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float*
     return hip_status();
 }
 
+int32_t swarm_critic_state_range(swarm_handle_t* h, const swarm_state_t* state, int32_t env0, int32_t env_n,
+                                 float* out, void* stream) {
+    if (!h || !state || !state->pos_x || !state->pos_y || !state->yaw || !out) return SWARM_ERR_ARG;
+    if (env0 < 0 || env_n < 1 || (int64_t)env0 + env_n > h->p.num_envs) return SWARM_ERR_ARG;
+    Geom g = h->g;
+    g.E = env_n;   // critic5 reads only the geometry constants; E bounds the launch
+    const size_t o = (size_t)env0 * (size_t)h->p.num_agents;
+    launch_critic(g, state->pos_x + o, state->pos_y + o, state->yaw + o, out, (hipStream_t)stream);
+    return hip_status();
+}
+
 // FSM word: three 8-bit fields at bits 0 (exploration), 8 (phototaxis),
 // 16 (anti-phototaxis); each = state(1) | steps(4, two's complement) << 1 |
 // dir(2, two's complement: +1 = 01, -1 = 11, 0 = 00) << 5.

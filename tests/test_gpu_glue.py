@@ -147,8 +147,9 @@ def _reference_loop(env, actor, critic, buf, obs_dict, R, dp, strength):
     return glue
 
 
+@pytest.mark.parametrize("groups", [1, 2, 3])   # 2, 3: the pipelined loop (env groups on their own streams)
 @pytest.mark.parametrize("steps_before", [0, 1185])  # mid-episode / crossing the 1200-step time-out
-def test_collector_matches_substep_loop(gpu_device, steps_before):
+def test_collector_matches_substep_loop(gpu_device, steps_before, groups):
     E, R, dp = 64, 6, 5
     torch.manual_seed(0)
     actor, critic = _Actor(24).to(gpu_device), _Critic().to(gpu_device)
@@ -170,8 +171,10 @@ def test_collector_matches_substep_loop(gpu_device, steps_before):
     with torch.no_grad():
         glue = _reference_loop(envs[0], actor, critic, bufs[0], obs0[0], R, dp, 0.5)
     torch.manual_seed(1)
-    col = POCARolloutCollector(envs[1], bufs[1], actor, critic, decision_period=dp, reward_strength=0.5)
+    col = POCARolloutCollector(envs[1], bufs[1], actor, critic, decision_period=dp, reward_strength=0.5,
+                               groups=groups)
     col.collect(torch.stack([obs0[1][a] for a in envs[1].possible_agents], dim=1), R)
+    torch.cuda.synchronize(gpu_device)
     ref, got = bufs[0], bufs[1]
     for k in ("obs", "critic_states", "actions", "log_probs", "rewards", "dones", "timeouts", "timeout_values",
               "team_values", "baselines", "returns", "advantages"):
@@ -181,6 +184,46 @@ def test_collector_matches_substep_loop(gpu_device, steps_before):
     assert ret == glue.returns and length == glue.lengths and group == glue.group
     if steps_before:
         assert len(ret) == E  # every env timed out once inside the rollout
+
+
+def test_pipelined_collector_with_poca_networks(gpu_device):
+    """The pipelined decision loop (groups 2 and 4: each env group's actor MLP, sample, critic
+    attention and step on its own stream, no per-decision join) with the real dandelion networks
+    (poca_networks.Actor, POCACritic) fills the rollout buffer, the completed-episode log and the
+    returns bit for bit as the one-stream loop, across the 1200-step time-out."""
+    from SwarmACB_isaac.agents.poca_networks import Actor, POCACritic
+
+    E, R, dp = 96, 8, 5
+    torch.manual_seed(0)
+    actor = Actor(24, 2, 64, 2).to(gpu_device)
+    critic = POCACritic(5, 2, 20, 128, 4, 1).to(gpu_device)   # the fused critic attention (h 128)
+    results = []
+    for groups in (1, 2, 4):
+        cfg = HomingEnvCfg()
+        cfg.scene.num_envs, cfg.seed = E, 4
+        env = make("SwarmACB-Homing-v0", cfg, device=gpu_device)
+        buf = POCARolloutBuffer(R, E, 20, obs_dim=24, act_dim=2, device=gpu_device)
+        obs_dict, _ = env.reset()
+        for _ in range(1180):
+            obs_dict, *_ = env.step(torch.zeros(E, 20, 2, device=gpu_device))
+        torch.manual_seed(11)
+        col = POCARolloutCollector(env, buf, actor, critic, decision_period=dp, groups=groups)
+        last = col.collect(torch.stack([obs_dict[a] for a in env.possible_agents], dim=1), R)
+        torch.cuda.synchronize(gpu_device)
+        results.append(({k: getattr(buf, k)[:R].cpu().numpy() for k in (
+            "obs", "critic_states", "actions", "log_probs", "rewards", "dones", "timeouts", "timeout_values",
+            "team_values", "baselines", "returns", "advantages")}, col.recorder.drain(), last.cpu().numpy(),
+            env.engine.dump_state()))
+        env.close()
+    ref = results[0]
+    assert len(ref[1][0]) == E          # every env timed out once inside the rollout
+    for groups, got in zip((2, 4), results[1:]):
+        for k in ref[0]:
+            np.testing.assert_array_equal(got[0][k], ref[0][k], err_msg=f"groups={groups}: {k}")
+        assert got[1] == ref[1], f"groups={groups}: completed-episode log"
+        np.testing.assert_array_equal(got[2], ref[2])
+        for k in ref[3]:
+            np.testing.assert_array_equal(got[3][k], ref[3][k], err_msg=f"groups={groups}: env state {k}")
 
 
 def _reference_loop_recurrent(env, actor, critic, buf, obs_dict, R, dp, strength, mem):

@@ -97,12 +97,49 @@ def reference_loop(env, actor, critic, buf, obs_dict, R, dp, mem):
     buf.compute_returns_and_advantages(critic.critic_pass(env.get_critic_state(), (mem["ch"], mem["cc"])).squeeze(-1))
 
 
+def dandelion(args):
+    """The C2-shaped rollout (Homing dandelion: Gaussian MLP actor, POCA attention critic, 24-D obs,
+    continuous wheels) through POCARolloutCollector with `--groups` env groups: groups > 1 is the
+    pipelined loop whose step schedule `bench.py --groups` times (each group's decisions an
+    independent chain on its own stream)."""
+    from SwarmACB_isaac import HomingEnvCfg
+    from SwarmACB_isaac.agents.poca_networks import Actor
+
+    E, N, dp, R = args.envs, 20, 5, args.decisions
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    actor = Actor(24, 2, 256, 2).to(dev)
+    critic = POCACritic(5, 2, N, 128, 4, 1).to(dev)
+    cfg = HomingEnvCfg()
+    cfg.scene.num_envs, cfg.seed = E, 1
+    env = make("SwarmACB-Homing-v0", cfg, device=dev)
+    buf = POCARolloutBuffer(R + 2, E, N, obs_dim=24, act_dim=2, device=dev)
+    col = POCARolloutCollector(env, buf, actor, critic, decision_period=dp, groups=args.groups)
+    obs_dict, _ = env.reset()
+    obs = torch.stack([obs_dict[a] for a in env.possible_agents], dim=1)
+    obs = col.collect(obs, 2)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    col.collect(obs, R)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / R * 1e3
+    print(json.dumps({"stage": "rollout_decision", "variant": "dandelion", "groups": args.groups,
+                      "ms_per_decision": ms, "agent_steps_per_s": E * N * dp / (ms * 1e-3),
+                      "config": {"workload": "Homing dandelion MA-POCA rollout: Actor MLP 2x256 + POCA attention "
+                                             "critic (h 128, 4 heads) + env + buffer", "num_envs": E,
+                                 "num_agents": N, "decision_period": dp, "decisions": R}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=8192)
     ap.add_argument("--decisions", type=int, default=24)
     ap.add_argument("--ref-decisions", type=int, default=6)
+    ap.add_argument("--variant", default="cyclamen", choices=("cyclamen", "dandelion"))
+    ap.add_argument("--groups", type=int, default=1, help="dandelion: env groups of the pipelined loop")
     args = ap.parse_args()
+    if args.variant == "dandelion":
+        return dandelion(args)
     E, N, dp, R = args.envs, 20, 5, args.decisions
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
