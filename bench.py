@@ -358,6 +358,8 @@ def main():
             sys.exit(2)
         sys.path.insert(0, os.path.join(ROOT, "tools"))
         sys.argv = [sys.argv[0]] + args.rest
+        if args.collect and args.groups != 1:
+            sys.argv += ["--groups", str(args.groups)]   # the pipelined collector's env groups
         if args.train:
             import bench_train
 

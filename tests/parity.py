@@ -250,6 +250,29 @@ def reproduced_by(key: str, v, spread: dict, idx: tuple) -> list[str]:
     return names
 
 
+def nearest_outcome(key: str, v, spread: dict, idx: tuple) -> tuple[str, float]:
+    """The oracle run ("plain" or a PERTURBATIONS name) whose output at element idx is nearest to
+    v, and that distance (angles modulo 2 pi): which 1-ulp perturbation reproduces a value that
+    passed through the envelope."""
+    b = float(np.asarray(spread[key + "@base"])[idx])
+    off = float(_signed(key, np.asarray(v, np.float64)[idx], b))
+    wrap = _angle_mask(key, np.shape(spread[key + "@base"])) is not None
+
+    def dist(o):
+        d = abs(off - o)
+        return min(d, abs(d - TWO_PI)) if wrap else d
+
+    best = ("plain", dist(0.0))
+    for p, o in zip(PERTURBATIONS, spread.get(key + "@outs", ())):
+        d = dist(float(np.asarray(o)[idx]))
+        if d < best[1]:
+            best = (p, d)
+    return best
+
+
+LARGE_ENVELOPE_DELTA = 1e-4   # envelope-only elements above this |delta| are listed with their perturbation
+
+
 def float_verdict(key: str, g, r, spread: dict | None):
     """(ok, plain_ok, hull_only) element masks of the fp32 rule in the module docstring."""
     d = _delta(key, g, r)
@@ -299,6 +322,7 @@ def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = 
             stats.setdefault(c, 0)
         stats.setdefault("envelope_max_delta", {})
         stats.setdefault("hull_examples", [])
+        stats.setdefault("large_envelope_examples", [])
     for k in keys:
         if k not in got or k not in ref:
             continue
@@ -318,8 +342,19 @@ def compare(got: dict, ref: dict, spread: dict, keys=None, stats: dict | None = 
                 stats["spread_capped_elements"] += int((sp > SPREAD_CAP).sum())
                 cont_only = env_only & ~hull_only
                 if cont_only.any():
-                    dmax = float(_delta(k, g, r)[cont_only].max())
+                    dd = _delta(k, g, r)
+                    dmax = float(dd[cont_only].max())
                     stats["envelope_max_delta"][k] = max(stats["envelope_max_delta"].get(k, 0.0), dmax)
+                    big = cont_only & (dd > LARGE_ENVELOPE_DELTA)
+                    for idx in np.argwhere(big)[:max(0, HULL_EXAMPLES - len(stats["large_envelope_examples"]))]:
+                        idx = tuple(int(i) for i in idx)
+                        gp, gd = nearest_outcome(k, g, spread, idx) if (k + "@base") in spread else ("", -1.0)
+                        rp, rd = nearest_outcome(k, r, spread, idx) if (k + "@base") in spread else ("", -1.0)
+                        stats["large_envelope_examples"].append(
+                            {"key": k, "index": list(idx), "got": float(g[idx]), "ref": float(r[idx]),
+                             "delta": float(dd[idx]), "spread": float(sp[idx]),
+                             "got_nearest_run": gp, "got_nearest_dist": gd,
+                             "ref_nearest_run": rp, "ref_nearest_dist": rd})
                 for idx in np.argwhere(hull_only)[:max(0, HULL_EXAMPLES - len(stats["hull_examples"]))]:
                     idx = tuple(int(i) for i in idx)
                     b = spread[k + "@base"][idx]
@@ -366,9 +401,41 @@ def merge_stats(stats_list: list[dict]) -> dict:
     return tot
 
 
+BOUNDS_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "parity_bounds.json")
+_SEEN = {"hull_elements": 0}
+
+
+def tripwire(test: str, stats: dict, bounds: dict | None = None, seen: dict | None = None):
+    """Fail when the envelope grows past the committed record (tests/parity_bounds.json, the
+    maxima of the HEAD record profiles/r06/parity_envelope.json): the suite's running count of
+    hull-rule elements may not exceed `hull_elements_max`, and no test group's largest
+    envelope-only |delta| per key may exceed the recorded one. GPU groups only (the CPU oracle
+    group, oracle_vs_reference, has its own fixtures' bar)."""
+    import json
+
+    if bounds is None:
+        if not os.path.exists(BOUNDS_PATH):
+            return
+        with open(BOUNDS_PATH) as f:
+            bounds = json.load(f)
+    seen = _SEEN if seen is None else seen
+    group = test.split("/")[0]
+    if not group.startswith("gpu_"):
+        return
+    seen["hull_elements"] = seen.get("hull_elements", 0) + int(stats.get("hull_elements", 0))
+    if seen["hull_elements"] > bounds["hull_elements_max"]:
+        raise AssertionError(f"parity tripwire: {seen['hull_elements']} hull-rule elements so far in this run "
+                             f"(after {test}), the record allows {bounds['hull_elements_max']}")
+    lim = bounds["envelope_max_delta"].get(group, {})
+    for k, v in stats.get("envelope_max_delta", {}).items():
+        if v > lim.get(k, 0.0):
+            raise AssertionError(f"parity tripwire: {test}: envelope-only |delta| of {k} = {v:.3g} exceeds the "
+                                 f"recorded {lim.get(k, 0.0):.3g} of group {group}")
+
+
 def record_stats(test: str, stats: dict):
     """Print a test's envelope counts and append them to gpurun_out/parity_stats.jsonl
-    (when that directory exists: the GPU runs bring it back)."""
+    (when that directory exists: the GPU runs bring it back); then the tripwire."""
     import json
 
     print(f"[parity] {test}: {stats}")
@@ -376,6 +443,8 @@ def record_stats(test: str, stats: dict):
     if os.path.isdir(out):
         with open(os.path.join(out, "parity_stats.jsonl"), "a") as f:
             f.write(json.dumps({"test": test, **stats}) + "\n")
+    if os.environ.get("SWARM_PARITY_TRIPWIRE", "1") != "0":
+        tripwire(test, stats)
 
 
 # --------------------------------------------------------------------------
@@ -469,7 +538,7 @@ def check_kernel_step(cfg: tuple, before: dict, actions, draws: dict, got: dict)
     stats = {"elements": int(sum(np.asarray(v).size for k, v in ref.items() if k in got)),
              "envs_needing_envelope": 0, "spread_only_elements": 0, "discrete_exempt_elements": 0,
              "spread_capped_elements": 0, "hull_elements": 0, "envs_sensor_stage": 0,
-             "envelope_max_delta": {}, "hull_examples": []}
+             "envelope_max_delta": {}, "hull_examples": [], "large_envelope_examples": []}
     bad = _bad_envs(got, ref, None, E)
     if not bad.any():
         return [], stats

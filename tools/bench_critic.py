@@ -95,15 +95,21 @@ def main():
     # as 16x16x4 f32 MFMAs (2048 flops each); the state-row term is VALU
     tiles = lambda a: (a + 15) // 16  # noqa: E731
     mfmas = H * tiles(R) ** 2 * (h // H // 4) + tiles(R) * (h // 16) * (h // 4) + H * (N * N // 16) * (h // 16) * (N // 4)
+    executed = E * mfmas * 2048.0
     print(json.dumps({"stage": "rsa_pool_kernel", "ms": sec * 1e3, "algorithmic_flops": flops,
-                      "executed_mfma_flops": E * mfmas * 2048.0,
-                      "roofline": {"bound": "mfma", "achieved": flops / sec / 1e12, "peak": MFMA_F32_PEAK,
-                                   "unit": "TFLOP/s", "frac": flops / sec / 1e12 / MFMA_F32_PEAK,
-                                   "executed_mfma_tflops": E * mfmas * 2048.0 / sec / 1e12,
+                      "executed_mfma_flops": executed,
+                      # the roofline of record counts the flops the kernel EXECUTES (Weak 4):
+                      # fc_out is folded into the values, so the reference formulation's flops exceed
+                      # the work done; that figure stays as a secondary field
+                      "roofline": {"bound": "mfma", "achieved": executed / sec / 1e12, "peak": MFMA_F32_PEAK,
+                                   "unit": "TFLOP/s", "frac": executed / sec / 1e12 / MFMA_F32_PEAK,
+                                   "flops": "executed (16x16x4 f32 MFMAs issued x 2048)",
+                                   "reference_formulation_tflops": flops / sec / 1e12,
+                                   "reference_formulation_frac": flops / sec / 1e12 / MFMA_F32_PEAK,
                                    # logits, P.V and fc_out all run on v_mfma_f32_16x16x4_f32
                                    "mfma_share_of_flops": 1.0},
-                      "note": "achieved = the reference algorithm's flops / kernel time; the kernel "
-                              "executes executed_mfma_flops (fc_out folded into the values)",
+                      "note": "achieved / frac = executed MFMA flops / kernel time; reference_formulation_* = "
+                              "the reference algorithm's flops (fc_out applied per set) / kernel time",
                       "config": cfg}), flush=True)
 
     if args.kernel_only:
