@@ -250,7 +250,7 @@ class POCARolloutCollector:
             last_tv = self.critic.critic_pass(last_state, (self.critic_memory_h, self.critic_memory_c)).squeeze(-1)
         else:
             last_tv = self.critic.critic_pass(last_state).squeeze(-1)
-        buf.compute_returns_and_advantages(last_tv)
+        self.buffer.compute_returns_and_advantages(last_tv)
         return obs.clone()
 
     def _collect_pipelined(self, obs: torch.Tensor, rollout_steps: int) -> torch.Tensor:

@@ -186,11 +186,15 @@ def test_collector_matches_substep_loop(gpu_device, steps_before, groups):
         assert len(ret) == E  # every env timed out once inside the rollout
 
 
+CRITIC_KEYS = ("timeout_values", "team_values", "baselines", "returns", "advantages")
+
+
 def test_pipelined_collector_with_poca_networks(gpu_device):
     """The pipelined decision loop (groups 2 and 4: each env group's actor MLP, sample, critic
     attention and step on its own stream, no per-decision join) with the real dandelion networks
-    (poca_networks.Actor, POCACritic) fills the rollout buffer, the completed-episode log and the
-    returns bit for bit as the one-stream loop, across the 1200-step time-out."""
+    (poca_networks.Actor, POCACritic) against the one-stream loop, across the 1200-step time-out:
+    observations, env state, actions, log-probs, rewards, dones and the completed-episode log bit
+    for bit; the critic's values (and the returns built on them) to 1e-6 (a smaller GEMM)."""
     from SwarmACB_isaac.agents.poca_networks import Actor, POCACritic
 
     E, R, dp = 96, 8, 5
@@ -219,7 +223,13 @@ def test_pipelined_collector_with_poca_networks(gpu_device):
     assert len(ref[1][0]) == E          # every env timed out once inside the rollout
     for groups, got in zip((2, 4), results[1:]):
         for k in ref[0]:
-            np.testing.assert_array_equal(got[0][k], ref[0][k], err_msg=f"groups={groups}: {k}")
+            if k in CRITIC_KEYS:
+                # a group's critic GEMMs run over fewer rows, and the library may pick another
+                # tiling for that shape: the values agree to an ulp, not bit for bit
+                np.testing.assert_allclose(got[0][k], ref[0][k], rtol=1e-6, atol=1e-7,
+                                           err_msg=f"groups={groups}: {k}")
+            else:
+                np.testing.assert_array_equal(got[0][k], ref[0][k], err_msg=f"groups={groups}: {k}")
         assert got[1] == ref[1], f"groups={groups}: completed-episode log"
         np.testing.assert_array_equal(got[2], ref[2])
         for k in ref[3]:
