@@ -50,7 +50,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1200, help="timed env.steps (physics updates)")
     ap.add_argument("--warmup", type=int, default=50, help="untimed env.steps")
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (step bench default 4096; passed on to "
+                                                            "--collect / --rollout / --critic / --train when given)")
     ap.add_argument("--decision-period", type=int, default=5)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo")
@@ -360,6 +361,8 @@ def main():
         sys.argv = [sys.argv[0]] + args.rest
         if args.collect and args.groups != 1:
             sys.argv += ["--groups", str(args.groups)]   # the pipelined collector's env groups
+        if args.envs is not None:
+            sys.argv += ["--envs", str(args.envs)]
         if args.train:
             import bench_train
 
@@ -412,7 +415,7 @@ def main():
     from SwarmACB_isaac.engine import SwarmEngine
     from SwarmACB_isaac.shard import EnvShard, max_over_ranks
 
-    E, dp = args.envs, args.decision_period
+    E, dp = args.envs or 4096, args.decision_period
     shard = EnvShard.weak(E, rank, world)     # weak scaling: E envs per GPU, keyed by global env id
     eng = SwarmEngine("homing", "isaac", E, N_AGENTS, 24, False, 1200, 1, shard.env_offset, args.seed, dev,
                       layout=args.layout or None)
@@ -448,7 +451,6 @@ def main():
     # --graph 1: the timed decisions are captured once as a HIP graph and replayed behind the
     # gate (the timing events stay outside the capture: ROCm refuses external events in one).
     stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     graph = None
     if args.graph and streams is not None:
         print("bench.py: --graph with --groups > 1 is not supported", file=sys.stderr, flush=True)
@@ -466,24 +468,26 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # the streams the timed launches run on: the current stream, or the K group streams, each of
+    # which gets its own gate and start / end events (no cross-stream event inside the region:
+    # a fork / join between queues adds signalling latency the short driver run would count)
+    run_streams = streams if streams is not None else [stream]
+    starts = [torch.cuda.Event(enable_timing=True) for _ in run_streams]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in run_streams]
     if gate is not None:
         flag.value = 0
         C.c_uint32.from_address(gate.value + 4).value = 0
-        _native.check(eng.lib.swarm_gate_wait(gate, 10_000_000, C.c_void_p(stream.cuda_stream)), "swarm_gate_wait")
-    ev0.record(stream)
-    if streams is not None:
-        # one fork at the start (the group streams wait for the gate / ev0) and one join at the end
-        for st_k in streams:
-            st_k.wait_stream(stream)
+        for st_k in run_streams:
+            _native.check(eng.lib.swarm_gate_wait(gate, 10_000_000, C.c_void_p(st_k.cuda_stream)), "swarm_gate_wait")
+    for st_k, ev in zip(run_streams, starts):
+        ev.record(st_k)
     if graph is not None:
         graph.replay()
     else:
         for d in range(n_dec):
             eng.step(acts[n_warm + d], dp, out=out, streams=streams)
-    if streams is not None:
-        for st_k in streams:
-            stream.wait_stream(st_k)
-    ev1.record(stream)
+    for st_k, ev in zip(run_streams, ends):
+        ev.record(st_k)
     t0 = time.perf_counter()
     if gate is not None:
         flag.value = 1
@@ -498,7 +502,9 @@ def main():
         # t0 and the wall clock would miss them)
         gate_timed_out = C.c_uint32.from_address(gate.value + 4).value != 0
         _native.check(eng.lib.swarm_gate_free(gate), "swarm_gate_free")
-    region_s = ev0.elapsed_time(ev1) / 1e3
+    # GPU region: earliest start to latest end over the streams (events are device timestamps)
+    first = starts[0]
+    region_s = (max(first.elapsed_time(e) for e in ends) - min(first.elapsed_time(e) for e in starts)) / 1e3
     avg_kernel_s = region_s / n_dec
     if gate_timed_out or elapsed < 0.98 * region_s:
         print(f"bench.py: rank {rank}: invalid timed region (gate timed out: {gate_timed_out}; wall "
