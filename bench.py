@@ -491,10 +491,15 @@ def main():
     t0 = time.perf_counter()
     if gate is not None:
         flag.value = 1
+    # the wall clock stops when the host sees every stream's end event complete (a spin on the
+    # events: a blocking device synchronize adds a wake-up latency of up to ~80 us, measured on
+    # the driver's 4-decision region, profiles/r06/groups/)
+    while not all(e.query() for e in ends):
+        pass
+    elapsed = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     gate_timed_out = False
     if gate is not None:
         # word 1 of the gate buffer: set by gate_kernel when it released on its timeout instead
@@ -525,7 +530,7 @@ def main():
         pmc, pmc_why = load_pmc(E, dp, lib_path)
         traffic = pmc.get("hbm_bytes_per_launch")
         roofline = valu_roofline(pmc, pmc_why, avg_kernel_s, achieved, traffic, E, dp, bytes_per_launch,
-                                 lib_sha256(lib_path) if lib_path else None, eng.layout, args.groups)
+                                 lib_sha256(lib_path) if lib_path else None, eng.split_layout(args.groups), args.groups)
         line = {
             "metric": METRIC,
             "value": value,
@@ -550,7 +555,7 @@ def main():
                 "num_agents": N_AGENTS,
                 "global_envs": world * E,
                 "decision_period": dp,
-                "layout": eng.layout,
+                "layout": eng.split_layout(args.groups),
                 "groups": args.groups,
                 "timed_launches": ("one HIP graph of the timed decisions, replayed once" if graph is not None
                                    else "eager launches" if streams is None

@@ -172,11 +172,13 @@ int32_t swarm_step_streams(swarm_handle_t* h, const swarm_state_t* state, const 
                            const float* override_wheels, const swarm_outputs_t* out, int32_t n_substeps,
                            const swarm_replay_t* replay, void* const* streams, int32_t n_groups);
 
-/* The work layout the handle's step launches use (103: one wave per arena, 3 lanes per robot;
- * 203: the two-wave pipeline of the continuous Isaac step; 4: the generic-N fallback), after
- * swarm_create's device-dependent choice for layout 0; -1 for a null handle. No reference
- * counterpart (bench.py labels its roofline line with it). */
-int32_t swarm_layout(const swarm_handle_t* h);
+/* The work layout the step launches use when a decision is split into n_groups env ranges
+ * (1 = swarm_step): 103 (one wave per arena, 3 lanes per robot), 203 (the two-wave pipeline of the
+ * continuous Isaac step) or 4 (the generic-N fallback). With layout 0 (auto) the creation rule is
+ * applied per launch: 203 when a launch's env range fits two waves per arena at 4 per SIMD
+ * (<= 8 x the device's CUs), else 103; -1 for a null handle or n_groups outside 1..8. No
+ * reference counterpart (bench.py labels its roofline line with it). */
+int32_t swarm_layout(const swarm_handle_t* h, int32_t n_groups);
 
 /* get_critic_state() (directional_gate_env.py:1279-1290 -> epuck_sensors.py:545-586): out [E*N*5]. */
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream);

@@ -167,7 +167,7 @@ def load() -> C.CDLL:
     lib.swarm_critic_state_range.argtypes = [C.c_void_p, C.POINTER(SwarmState), C.c_int32, C.c_int32, C.c_void_p,
                                              C.c_void_p]
     lib.swarm_layout.restype = C.c_int32
-    lib.swarm_layout.argtypes = [C.c_void_p]
+    lib.swarm_layout.argtypes = [C.c_void_p, C.c_int32]
     lib.swarm_fsm_pack.restype = C.c_uint32
     lib.swarm_fsm_pack.argtypes = [C.c_int32, C.c_int32, C.c_float] * 3
     i32, i64, vp = C.c_int32, C.c_int64, C.c_void_p

@@ -203,7 +203,11 @@ class SwarmEngine:
     @property
     def layout(self) -> int:
         """The step launches' work layout (swarm_layout: 103, 203 or 4)."""
-        return int(self.lib.swarm_layout(self.handle))
+        return int(self.lib.swarm_layout(self.handle, 1))
+
+    def split_layout(self, groups: int) -> int:
+        """The layout of each launch when a decision is split into `groups` env ranges."""
+        return int(self.lib.swarm_layout(self.handle, int(groups)))
 
     def critic_state(self, out: torch.Tensor | None = None) -> torch.Tensor:
         out = out if out is not None else torch.empty(self.E, self.N, 5, dtype=torch.float32, device=self.device)

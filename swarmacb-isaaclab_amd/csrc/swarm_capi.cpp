@@ -76,6 +76,10 @@ struct swarm_handle {
     hipStream_t gstream[SWARM_MAX_STEP_GROUPS] = {};
     hipEvent_t gjoin[SWARM_MAX_STEP_GROUPS] = {};
     hipEvent_t gfork = nullptr;
+    // layout 0 (auto) for a continuous Isaac step with 20 robots: each launch of swarm_step_streams
+    // picks 203 when its env range fits 2 waves per arena at 4 per SIMD (<= 8 x CUs), else 103
+    bool auto_pipe = false;
+    int cus = 0;
 };
 
 namespace {
@@ -147,9 +151,11 @@ int32_t swarm_create(const swarm_params_t* p, swarm_handle_t** out) {
         // occupancy an arena's dependent chain bounds layout 103's launch (swarm_step_impl.h)
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0 &&
-            (int64_t)p->num_envs <= (int64_t)cus * 4 * 2)
-            h->g.layout = 203;
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) {
+            h->auto_pipe = true;
+            h->cus = cus;
+            if ((int64_t)p->num_envs <= (int64_t)cus * 4 * 2) h->g.layout = 203;
+        }
     }
     // the kernels use the compile-time tables generated from this same build_geom
     // (gen_tables.cpp); refuse to run if the library was built from stale tables
@@ -289,6 +295,14 @@ Geom group_geom(const swarm_handle_t* h, int k, int K) {
     gk.env_n = (int32_t)((int64_t)E * (k + 1) / K) - gk.env0;
     return gk;
 }
+
+// the layout of one launch of a K-way split (swarm_step_streams): with layout 0 (auto) the
+// creation rule applied to the launch's env range (the largest range, E / K rounded up)
+int32_t split_layout(const swarm_handle_t* h, int K) {
+    if (!h->auto_pipe || K <= 1) return h->g.layout;
+    const int64_t n = ((int64_t)h->p.num_envs + K - 1) / K;
+    return n <= (int64_t)h->cus * 4 * 2 ? 203 : 103;
+}
 }  // namespace
 
 int32_t swarm_step(swarm_handle_t* h, const swarm_state_t* state, const void* actions, const float* override_wheels,
@@ -333,14 +347,21 @@ int32_t swarm_step_streams(swarm_handle_t* h, const swarm_state_t* state, const 
     const uint64_t reset_any = advance_mirror(h, n_substeps);
     const DevState st = dev_state(state);
     const DevOut o{out->obs, out->reward, out->truncated};
-    for (int k = 0; k < n_groups; ++k)
-        launch_step(n_groups > 1 ? group_geom(h, k, n_groups) : h->g, st, actions, override_wheels, o,
-                    dev_replay(replay), h->tick, n_substeps, reset_any, (hipStream_t)streams[k]);
+    const int32_t ly = split_layout(h, n_groups);
+    for (int k = 0; k < n_groups; ++k) {
+        Geom gk = n_groups > 1 ? group_geom(h, k, n_groups) : h->g;
+        gk.layout = ly;
+        launch_step(gk, st, actions, override_wheels, o, dev_replay(replay), h->tick, n_substeps, reset_any,
+                    (hipStream_t)streams[k]);
+    }
     h->tick += (uint64_t)n_substeps;
     return hip_status();
 }
 
-int32_t swarm_layout(const swarm_handle_t* h) { return h ? h->g.layout : -1; }
+int32_t swarm_layout(const swarm_handle_t* h, int32_t n_groups) {
+    if (!h || n_groups < 1 || n_groups > SWARM_MAX_STEP_GROUPS) return -1;
+    return split_layout(h, n_groups);
+}
 
 int32_t swarm_critic_state(swarm_handle_t* h, const swarm_state_t* state, float* out, void* stream) {
     if (!h || !state || !state->pos_x || !state->pos_y || !state->yaw || !out) return SWARM_ERR_ARG;

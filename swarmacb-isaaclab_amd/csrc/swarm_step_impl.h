@@ -1688,8 +1688,11 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // arena must fit 64 VGPRs: with the ray directions re-evaluated per use and the packet-loss draw
 // late it compiled to 64 with 18 spilled and ran 59 us against layout 103's 55 us at C2 - measured,
 // DESIGN.md §13; the variant is in git history.)
+#ifndef SWARM_PIPE_MIN_WAVES
+#define SWARM_PIPE_MIN_WAVES 4   // waves per SIMD the layout-203 register budget must allow
+#endif
 template <int MISSION>
-__global__ __launch_bounds__(128, 4) void step_kernel_pipe(
+__global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     const Geom gr, const DevState st, const void* __restrict__ actions, const DevOut out, uint64_t tick0, int n_sub,
     uint64_t reset_any) {
     constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;

@@ -90,11 +90,12 @@ def test_step_streams_argument_checks():
     """swarm_step_streams validates before touching the device; swarm_layout reports the handle's
     layout (103 for N = 20 when no GPU is there to pick 203)."""
     lib = _native.load()
-    assert lib.swarm_layout(None) == -1
+    assert lib.swarm_layout(None, 1) == -1
     h = C.c_void_p()
     assert lib.swarm_create(C.byref(_params(num_envs=4)), C.byref(h)) == 0
     try:
-        assert lib.swarm_layout(h) in (103, 203)
+        assert lib.swarm_layout(h, 1) in (103, 203)
+        assert lib.swarm_layout(h, 0) == -1 and lib.swarm_layout(h, 9) == -1
         st = _native.SwarmState(*([1] * 13))
         out = _native.SwarmOutputs(1, 1, 1)
         streams = (C.c_void_p * 8)()
