@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--gate", type=int, default=1,
                     help="1: the timed launches are enqueued behind a stream gate released after the enqueue "
                          "(swarm_gate_wait); 0: launched as they are enqueued")
-    ap.add_argument("--groups", type=int, default=1,
+    ap.add_argument("--groups", type=int, default=2,
                     help="env groups per GPU: each decision is K launches over contiguous env ranges on K "
                          "streams with no cross-stream ordering (swarm_step_streams): every range's decisions "
                          "form an independent chain, as in the pipelined collector")

@@ -25,6 +25,7 @@ What is MI355X-specific:
 from __future__ import annotations
 
 import itertools
+import os
 
 import torch
 import torch.optim as optim
@@ -92,7 +93,23 @@ class POCATrainer(TrainerBase):
         self.collector = POCARolloutCollector(
             env, self.buffer, self.actor, self.critic, decision_period=self.decision_period,
             reward_strength=self.reward_strength, discrete=self.discrete, num_actions=self.num_actions,
-            recurrent=self.recurrent)
+            recurrent=self.recurrent, groups=self._collect_groups(env))
+
+    def _collect_groups(self, env) -> int:
+        """Env groups of the pipelined decision loop (collector.py): SWARM_COLLECT_GROUPS, or by
+        default 2 where the loop applies (a SwarmEngine env, continuous non-recurrent actor, at
+        least 2 envs, episodes of >= 2 decisions): the step schedule `bench.py --groups 2` times."""
+        want = os.environ.get("SWARM_COLLECT_GROUPS")
+        engine = getattr(env, "engine", None)
+        ok = (engine is not None and not self.discrete and not self.recurrent and self.num_envs >= 2
+              and engine.max_episode_length >= 2 * self.decision_period)
+        if want is not None:
+            k = int(want)
+            if k > 1 and not ok:
+                raise ValueError("SWARM_COLLECT_GROUPS > 1 needs a SwarmEngine env with a continuous, "
+                                 "non-recurrent actor")
+            return max(1, k)
+        return 2 if ok else 1
 
     # ------------------------------------------------------------ reference attribute surface
     @property

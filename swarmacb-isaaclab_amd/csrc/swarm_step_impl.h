@@ -38,6 +38,13 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
+// SWARM_DISC_BITS=1 (measured variant): the proximity disc rays per lane by the
+// set bits of its own hit mask (a divergent loop over <= 2-3 rays) with the readings maxed into
+// per-lane LDS slots, instead of every ray the wave's lanes can hit between them.
+#ifndef SWARM_DISC_BITS
+#define SWARM_DISC_BITS 0
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -238,6 +245,10 @@ struct Shared {
     float4 seg[16];     // raycast segments (arena faces, internal walls): start (x, y), vector (x, y)
     float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
     int wsec[24];       // wall_sector3
+#if SWARM_DISC_BITS
+    float2 adir[8];                              // IR ray angles (cos_a, sin_a), body frame
+    uint32_t dmax[8][64 * ly_waves(LY)];        // per-lane disc-ray maxima (non-negative floats)
+#endif
 };
 
 
@@ -266,6 +277,9 @@ __device__ __forceinline__ void stage_tables(const Geom& g, SH& S, int t = -1) {
     if (t < 12) S.wface[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_px[t], g.face_py[t]);
     if (t < 24) S.wsec[t] = g.wall_sector3[t];
     if (t < 15) S.seg[t] = make_float4(g.seg_ax[t], g.seg_ay[t], g.seg_sx[t], g.seg_sy[t]);
+#if SWARM_DISC_BITS
+    if (t < 8) S.adir[t] = make_float2(g.cos_a[t], g.sin_a[t]);
+#endif
     (void)g;
     (void)S;
     (void)t;
@@ -717,9 +731,10 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
 template <int LY, int C, class SH>
-__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const SH& S, float x, float y,
+__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, SH& S, float x, float y,
                                                   const float rdx[8], const float rdy[8], float prox[8],
-                                                  const uint32_t* disc_cand = nullptr) {
+                                                  const uint32_t* disc_cand = nullptr, float cyw = 1.0f,
+                                                  float syw = 0.0f) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length.
@@ -804,10 +819,46 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         const uint32_t cand = disc_cand ? *disc_cand
                                         : chunk_mask<C>(L, S.xy, x, y,
                                                         [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
+#if SWARM_DISC_BITS
+        // the same hit tests per ray; only the rays THIS lane's disc passes the pre-test for are
+        // evaluated (the set bits of its own mask: <= 2 for a disc farther than 0.068 m, whose
+        // angular half-width is < 31 degrees against >= 32-degree ray gaps), the readings maxed into
+        // this lane's LDS slots (a reading is a non-negative float: its bits order as unsigned).
+        // The ray direction of bit k is re-evaluated with observe()'s expression: bitwise rdx[k], rdy[k].
+#pragma unroll
+        for (int k = 0; k < 8; ++k) S.dmax[k][L.tid] = 0u;
+        for_each_cand(L, S.xy, cand, [&](int, float2 p) {
+            SWARM_WT(L.wt_disc++);
+            const float dx = p.x - x, dy = p.y - y;
+            const float dsq = dx * dx + dy * dy;
+            uint32_t m = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float proj = rdx[k] * dx + rdy[k] * dy;
+                const float csq = dsq - proj * proj;
+                m |= ((proj > 0.0f) & (csq <= g.r2)) ? (1u << k) : 0u;
+            }
+            while (m) {
+                const int k = __builtin_ctz(m);
+                m &= m - 1u;
+                const float2 a = S.adir[k];
+                const float rx = a.x * cyw - a.y * syw, ry = a.x * syw + a.y * cyw;
+                const float proj = rx * dx + ry * dy;
+                const float csq = dsq - proj * proj;
+                const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
+                const float hd = fmaxf(proj - hc, 0.0f);
+                const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
+                if (hd <= g.prox_range) atomicMax(&S.dmax[k][L.tid], __float_as_uint(rv));
+            }
+        });
+#pragma unroll
+        for (int k = 0; k < 8; ++k) prox[k] = fmaxf(prox[k], __uint_as_float(S.dmax[k][L.tid]));
+#else
         for_each_cand(L, S.xy, cand, [&](int, float2 p) {
             SWARM_WT(L.wt_disc++);
             disc(p.x - x, p.y - y);
         });
+#endif
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -1257,7 +1308,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, flo
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr);
+        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr, cyw, syw);
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
@@ -1688,8 +1739,12 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // arena must fit 64 VGPRs: with the ray directions re-evaluated per use and the packet-loss draw
 // late it compiled to 64 with 18 spilled and ran 59 us against layout 103's 55 us at C2 - measured,
 // DESIGN.md §13; the variant is in git history.)
+// Waves per SIMD the layout-203 register budget must allow: 5 (96 VGPRs, no spill). The natural
+// allocation (100 VGPRs) held 4; the fifth resident wave is what a decision split into env groups
+// on streams (swarm_step_streams) fills the SIMDs with: C2 with 2 groups 8.15 -> 9.12e9
+// agent-steps/s; 6 waves (80 VGPRs, 52 B of scratch) 8.6e9.
 #ifndef SWARM_PIPE_MIN_WAVES
-#define SWARM_PIPE_MIN_WAVES 4   // waves per SIMD the layout-203 register budget must allow
+#define SWARM_PIPE_MIN_WAVES 5
 #endif
 template <int MISSION>
 __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
