@@ -180,7 +180,8 @@ def lib_sha256(path: str) -> str | None:
         return None
 
 
-def load_pmc(envs: int, sub: int, lib_path: str | None, path: str | None = None) -> tuple[dict, str | None]:
+def load_pmc(envs: int, sub: int, lib_path: str | None, path: str | None = None,
+             groups: int = 1) -> tuple[dict, str | None]:
     """Per-launch HBM bytes and VALU instruction count of the step kernel from the
     committed rocprofv3 PMC record (profiles/pmc_traffic.json, tools/pmc.sh).
 
@@ -194,8 +195,9 @@ def load_pmc(envs: int, sub: int, lib_path: str | None, path: str | None = None)
             d = json.load(f)
     except (OSError, ValueError) as e:
         return {}, f"no PMC record ({type(e).__name__})"
-    if d.get("envs") != envs or d.get("substeps") != sub:
-        return {}, f"PMC record taken at envs={d.get('envs')} substeps={d.get('substeps')}, not {envs} / {sub}"
+    if d.get("envs") != envs or d.get("substeps") != sub or d.get("groups", 1) != groups:
+        return {}, (f"PMC record taken at envs={d.get('envs')} substeps={d.get('substeps')} "
+                    f"groups={d.get('groups', 1)}, not {envs} / {sub} / {groups}")
     want = d.get("lib_sha256")
     have = lib_sha256(lib_path) if lib_path else None
     if not want:
@@ -311,7 +313,7 @@ def valu_roofline(pmc: dict, pmc_why: str | None, avg_kernel_s: float, hbm_achie
     (algorithmic bytes / kernel time, and the PMC traffic) is the secondary roof. The VALU
     count and the traffic come from the PMC record only when it was taken on the loaded
     library (load_pmc); otherwise they are null and `pmc_status` says why."""
-    valu_insts = pmc.get("valu_insts_per_launch")
+    valu_insts = pmc.get("valu_insts_per_decision", pmc.get("valu_insts_per_launch"))
     lane_ops = valu_insts * 64.0 if valu_insts else None
     achieved = lane_ops / avg_kernel_s / 1e12 if lane_ops else None
     return {
@@ -321,7 +323,7 @@ def valu_roofline(pmc: dict, pmc_why: str | None, avg_kernel_s: float, hbm_achie
         "unit": "T lane-ops/s",
         "frac": (lane_ops / avg_kernel_s / VALU_PEAK_LANE_OPS) if lane_ops else None,
         "traffic": traffic,
-        "valu_insts_per_launch": valu_insts,
+        "valu_insts_per_decision": valu_insts,
         "valu_busy": pmc.get("valu_busy"),
         "sq_wait_any_frac": pmc.get("sq_wait_any_frac"),
         "pmc_status": "ok" if pmc_why is None else pmc_why,
@@ -527,8 +529,9 @@ def main():
         bytes_per_launch = ALGO_BYTES_PER_AGENT_STEP * E * N_AGENTS * dp
         achieved = bytes_per_launch / avg_kernel_s / 1e9
         lib_path = getattr(eng.lib, "_name", None)
-        pmc, pmc_why = load_pmc(E, dp, lib_path)
-        traffic = pmc.get("hbm_bytes_per_launch")
+        pmc, pmc_why = load_pmc(E, dp, lib_path, groups=args.groups)
+        # per decision (= per launch when groups = 1): a decision is `groups` launches
+        traffic = pmc.get("hbm_bytes_per_decision", pmc.get("hbm_bytes_per_launch"))
         roofline = valu_roofline(pmc, pmc_why, avg_kernel_s, achieved, traffic, E, dp, bytes_per_launch,
                                  lib_sha256(lib_path) if lib_path else None, eng.split_layout(args.groups), args.groups)
         line = {

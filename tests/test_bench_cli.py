@@ -112,6 +112,18 @@ def test_load_pmc_requires_the_measured_library(tmp_path):
     assert d == {} and "stamp" in why
     d, why = bench.load_pmc(8192, 5, str(lib), _record(tmp_path, bench.lib_sha256(str(lib))))
     assert d == {} and "envs=4096" in why
+    # a record of the one-launch decision never feeds a 2-group line (per-decision figures differ)
+    d, why = bench.load_pmc(4096, 5, str(lib), _record(tmp_path, bench.lib_sha256(str(lib))), groups=2)
+    assert d == {} and "groups=1" in why
+
+
+def test_roofline_per_decision_with_groups():
+    """With groups, the record's per-decision figures (per-launch x groups) feed the line."""
+    pmc = {"groups": 2, "valu_insts_per_launch": 1.25e7, "valu_insts_per_decision": 2.5e7,
+           "hbm_bytes_per_decision": 2.2e7}
+    r = bench.valu_roofline(pmc, None, 50e-6, 1000.0, 2.2e7, 4096, 5, 5.28e7, "ab", 203, 2)
+    assert r["valu_insts_per_decision"] == 2.5e7 and r["groups"] == 2 and r["layout"] == 203
+    assert r["frac"] == pytest.approx(2.5e7 * 64 / 50e-6 / bench.VALU_PEAK_LANE_OPS)
 
 
 def test_roofline_line_shape():

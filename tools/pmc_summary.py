@@ -120,6 +120,9 @@ if __name__ == "__main__":
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--substeps", type=int, default=5)
     ap.add_argument("--layout", type=int, default=0)
+    ap.add_argument("--groups", type=int, default=1,
+                    help="env groups per decision of the measured bench (bench.py --groups): a decision is "
+                         "this many launches, so the per-decision figures are the per-launch averages x groups")
     ap.add_argument("--lib", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                                 "swarmacb-isaaclab_amd", "SwarmACB_isaac", "libswarmstep.so"),
                     help="the library the passes ran (its sha256 stamps the record)")
@@ -127,7 +130,10 @@ if __name__ == "__main__":
     o = main(a.root)
     if a.traffic_json:
         d = o["derived"]
-        rec = {"envs": a.envs, "substeps": a.substeps, "layout": a.layout,
+        per_dec = lambda v: None if v is None else v * a.groups  # noqa: E731
+        rec = {"envs": a.envs, "substeps": a.substeps, "layout": a.layout, "groups": a.groups,
+               "hbm_bytes_per_decision": per_dec(d.get("hbm_bytes_per_launch")),
+               "valu_insts_per_decision": per_dec(d.get("valu_insts_per_launch")),
                "hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"),
                "fetch_bytes_raw": d.get("fetch_bytes_raw"), "write_bytes": d.get("write_bytes"),
                "valu_insts_per_launch": d.get("valu_insts_per_launch"),
