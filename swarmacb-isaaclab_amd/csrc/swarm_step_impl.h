@@ -45,6 +45,14 @@
 #define SWARM_DISC_BITS 0
 #endif
 
+// SWARM_PAIR_COMPACT=1 (measured variant): the contact solver's candidate pairs of
+// an arena compacted over the wave (ballot + mbcnt), each unordered pair's term evaluated once by one
+// lane into an LDS pair table, and every robot lane summing its chunk's terms from the table in
+// increasing j (the same fp32 order as the per-lane loop).
+#ifndef SWARM_PAIR_COMPACT
+#define SWARM_PAIR_COMPACT 0
+#endif
+
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -235,7 +243,7 @@ __device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t bl
 // LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
 // broadcast within an arena) and 4 float4 partial slots per thread.
 // Slot use: 0 contact-solver sums, 0-1 proximity maxima, 2-3 range-and-bearing sums.
-template <int LY, int NRED = 4>
+template <int LY, int NRED = 4, bool PAIRS = true>
 struct Shared {
     float2 xy[64];
     int ins[64];
@@ -245,6 +253,10 @@ struct Shared {
     float4 seg[16];     // raycast segments (arena faces, internal walls): start (x, y), vector (x, y)
     float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
     int wsec[24];       // wall_sector3
+#if SWARM_PAIR_COMPACT
+    int plist[PAIRS ? 192 : 1];      // compacted contact pairs i | j << 8 (i < j) of the wave's arena
+    float2 pres[PAIRS ? 400 : 1];    // pair term (hx, hy) of pair (i, j), i < j, at i * 20 + j
+#endif
 #if SWARM_DISC_BITS
     float2 adir[8];                              // IR ray angles (cos_a, sin_a), body frame
     uint32_t dmax[8][64 * ly_waves(LY)];        // per-lane disc-ray maxima (non-negative floats)
@@ -461,11 +473,76 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, SH& S,
             return sq_dist(px, py, x, y, dx, dy) < g.min_dist_pre_lim;
         }, true);
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
+#if SWARM_PAIR_COMPACT
+        if constexpr (ly_parts(LY) == 3 && ly_waves(LY) == 1 && C == 7) {
+            // the candidate relation is symmetric (|p_i - p_j|^2 is bitwise sign-free), so every
+            // unordered candidate pair is the row entry (j > i) of exactly one lane: compact those
+            const int jrel = L.i - L.j0;                        // bits jj with j0 + jj > i
+            const uint32_t rowm = jrel < 0 ? 0x7Fu : (jrel >= 6 ? 0u : (0x7Fu & ~((2u << jrel) - 1u)));
+            const uint32_t row = cand & rowm;
+            const int cnt = __builtin_popcount(row);
+            const unsigned long long b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
+            const int U = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);   // wave-uniform
+            if (U == 0) {
+                x = (x + 0.0f) - 0.0f;
+                y = (y + 0.0f) - 0.0f;
+                return false;
+            }
+            auto below = [](unsigned long long b) {
+                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            };
+            const int pre = below(b0) + 2 * below(b1) + 4 * below(b2);
+#pragma unroll
+            for (int jj = 0; jj < C; ++jj) {
+                if ((row >> jj) & 1u)
+                    S.plist[pre + __builtin_popcount(row & ((1u << jj) - 1u))] = L.i | ((L.j0 + jj) << 8);
+            }
+            sync_wg<LY>();
+            for (int t = (int)(threadIdx.x & 63); __builtin_amdgcn_readfirstlane(t - (int)(threadIdx.x & 63)) < U;
+                 t += 64) {
+                if (t < U) {
+                    const int e = S.plist[t];
+                    const int ia = e & 255, jb = e >> 8;
+                    const float2 pa = S.xy[L.ab + ia], pb = S.xy[L.ab + jb];
+                    // pair_term of lane ia with neighbour jb (x = p_ia): bitwise what that lane computes
+                    float dx, dy;
+                    const float dd2 = sq_dist(pa.x, pa.y, pb.x, pb.y, dx, dy);
+                    const float dist = nsqrt(dd2 + 1e-8f);
+                    const float ov = g.min_dist - dist;
+                    const float inv = frcp(dist + 1e-8f);
+                    const float nx = dx * inv, ny = dy * inv;
+                    S.pres[ia * 20 + jb] = make_float2(ov * nx * 0.5f, ov * ny * 0.5f);
+                }
+            }
+            sync_wg<LY>();
+            // the per-lane loop's sums in increasing j: a row term (j > i) adds the pair's (hx, hy)
+            // to (rx, ry); a column term (j < i) adds -(hx, hy) of pair (i, j) = (hx, hy) of pair (j, i)
+            // (negated operands give negated products exactly) to (cx, cy)
+#pragma unroll
+            for (int jj = 0; jj < C; ++jj) {
+                const int j = L.j0 + jj;
+                if ((cand >> jj) & 1u) {
+                    const bool rw = j > L.i;
+                    const float2 v = S.pres[rw ? L.i * 20 + j : j * 20 + L.i];
+                    if (rw) {
+                        rx += v.x;
+                        ry += v.y;
+                    } else {
+                        cx += v.x;
+                        cy += v.y;
+                    }
+                }
+            }
+            SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
+        } else
+#endif
+        {
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
             pair_term(j, p, true);
         });
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
+        }
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -1753,7 +1830,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;
     const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
-    __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
+    __shared__ Shared<LY, 4, false> SO;   // observation: position tile, inside flags, partial slots, tables
     __shared__ float yaw_tile[64];
     const int lane = threadIdx.x & 63;
     const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
