@@ -38,21 +38,6 @@
 #include "swarm_geom.h"
 #include "swarm_launch.h"
 
-// SWARM_DISC_BITS=1 (measured variant): the proximity disc rays per lane by the
-// set bits of its own hit mask (a divergent loop over <= 2-3 rays) with the readings maxed into
-// per-lane LDS slots, instead of every ray the wave's lanes can hit between them.
-#ifndef SWARM_DISC_BITS
-#define SWARM_DISC_BITS 0
-#endif
-
-// SWARM_PAIR_COMPACT=1 (measured variant): the contact solver's candidate pairs of
-// an arena compacted over the wave (ballot + mbcnt), each unordered pair's term evaluated once by one
-// lane into an LDS pair table, and every robot lane summing its chunk's terms from the table in
-// increasing j (the same fp32 order as the per-lane loop).
-#ifndef SWARM_PAIR_COMPACT
-#define SWARM_PAIR_COMPACT 0
-#endif
-
 // Register budget: minimum resident waves per SIMD the compiler must allow.
 #ifndef SWARM_MIN_WAVES_PER_SIMD
 #define SWARM_MIN_WAVES_PER_SIMD 4
@@ -243,7 +228,7 @@ __device__ __forceinline__ uint4 rng4(const Lane& L, uint32_t robot, uint32_t bl
 // LDS of one workgroup: the position tile (one ds_read_b64 per neighbour,
 // broadcast within an arena) and 4 float4 partial slots per thread.
 // Slot use: 0 contact-solver sums, 0-1 proximity maxima, 2-3 range-and-bearing sums.
-template <int LY, int NRED = 4, bool PAIRS = true>
+template <int LY, int NRED = 4>
 struct Shared {
     float2 xy[64];
     int ins[64];
@@ -253,14 +238,6 @@ struct Shared {
     float4 seg[16];     // raycast segments (arena faces, internal walls): start (x, y), vector (x, y)
     float4 wface[12];   // arena faces: normal (x, y), anchor (x, y)
     int wsec[24];       // wall_sector3
-#if SWARM_PAIR_COMPACT
-    int plist[PAIRS ? 192 : 1];      // compacted contact pairs i | j << 8 (i < j) of the wave's arena
-    float2 pres[PAIRS ? 400 : 1];    // pair term (hx, hy) of pair (i, j), i < j, at i * 20 + j
-#endif
-#if SWARM_DISC_BITS
-    float2 adir[8];                              // IR ray angles (cos_a, sin_a), body frame
-    uint32_t dmax[8][64 * ly_waves(LY)];        // per-lane disc-ray maxima (non-negative floats)
-#endif
 };
 
 
@@ -289,9 +266,6 @@ __device__ __forceinline__ void stage_tables(const Geom& g, SH& S, int t = -1) {
     if (t < 12) S.wface[t] = make_float4(g.face_nx[t], g.face_ny[t], g.face_px[t], g.face_py[t]);
     if (t < 24) S.wsec[t] = g.wall_sector3[t];
     if (t < 15) S.seg[t] = make_float4(g.seg_ax[t], g.seg_ay[t], g.seg_sx[t], g.seg_sy[t]);
-#if SWARM_DISC_BITS
-    if (t < 8) S.adir[t] = make_float2(g.cos_a[t], g.sin_a[t]);
-#endif
     (void)g;
     (void)S;
     (void)t;
@@ -473,76 +447,11 @@ __device__ __forceinline__ bool robots_push(const Geom& g, const Lane& L, SH& S,
             return sq_dist(px, py, x, y, dx, dy) < g.min_dist_pre_lim;
         }, true);
         SWARM_PH_NEXT(L, PH_PUSH_CAND, wt_t);
-#if SWARM_PAIR_COMPACT
-        if constexpr (ly_parts(LY) == 3 && ly_waves(LY) == 1 && C == 7) {
-            // the candidate relation is symmetric (|p_i - p_j|^2 is bitwise sign-free), so every
-            // unordered candidate pair is the row entry (j > i) of exactly one lane: compact those
-            const int jrel = L.i - L.j0;                        // bits jj with j0 + jj > i
-            const uint32_t rowm = jrel < 0 ? 0x7Fu : (jrel >= 6 ? 0u : (0x7Fu & ~((2u << jrel) - 1u)));
-            const uint32_t row = cand & rowm;
-            const int cnt = __builtin_popcount(row);
-            const unsigned long long b0 = __ballot(cnt & 1), b1 = __ballot(cnt & 2), b2 = __ballot(cnt & 4);
-            const int U = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);   // wave-uniform
-            if (U == 0) {
-                x = (x + 0.0f) - 0.0f;
-                y = (y + 0.0f) - 0.0f;
-                return false;
-            }
-            auto below = [](unsigned long long b) {
-                return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-            };
-            const int pre = below(b0) + 2 * below(b1) + 4 * below(b2);
-#pragma unroll
-            for (int jj = 0; jj < C; ++jj) {
-                if ((row >> jj) & 1u)
-                    S.plist[pre + __builtin_popcount(row & ((1u << jj) - 1u))] = L.i | ((L.j0 + jj) << 8);
-            }
-            sync_wg<LY>();
-            for (int t = (int)(threadIdx.x & 63); __builtin_amdgcn_readfirstlane(t - (int)(threadIdx.x & 63)) < U;
-                 t += 64) {
-                if (t < U) {
-                    const int e = S.plist[t];
-                    const int ia = e & 255, jb = e >> 8;
-                    const float2 pa = S.xy[L.ab + ia], pb = S.xy[L.ab + jb];
-                    // pair_term of lane ia with neighbour jb (x = p_ia): bitwise what that lane computes
-                    float dx, dy;
-                    const float dd2 = sq_dist(pa.x, pa.y, pb.x, pb.y, dx, dy);
-                    const float dist = nsqrt(dd2 + 1e-8f);
-                    const float ov = g.min_dist - dist;
-                    const float inv = frcp(dist + 1e-8f);
-                    const float nx = dx * inv, ny = dy * inv;
-                    S.pres[ia * 20 + jb] = make_float2(ov * nx * 0.5f, ov * ny * 0.5f);
-                }
-            }
-            sync_wg<LY>();
-            // the per-lane loop's sums in increasing j: a row term (j > i) adds the pair's (hx, hy)
-            // to (rx, ry); a column term (j < i) adds -(hx, hy) of pair (i, j) = (hx, hy) of pair (j, i)
-            // (negated operands give negated products exactly) to (cx, cy)
-#pragma unroll
-            for (int jj = 0; jj < C; ++jj) {
-                const int j = L.j0 + jj;
-                if ((cand >> jj) & 1u) {
-                    const bool rw = j > L.i;
-                    const float2 v = S.pres[rw ? L.i * 20 + j : j * 20 + L.i];
-                    if (rw) {
-                        rx += v.x;
-                        ry += v.y;
-                    } else {
-                        cx += v.x;
-                        cy += v.y;
-                    }
-                }
-            }
-            SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
-        } else
-#endif
-        {
         for_each_cand(L, S.xy, cand, [&](int j, float2 p) {
             SWARM_WT(L.wt_pair++);
             pair_term(j, p, true);
         });
         SWARM_PH_NEXT(L, PH_PUSH_PAIRS, wt_t);
-        }
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -808,10 +717,9 @@ struct Agg {  // aggregates used by the behaviour modules (the DG sensor cache)
 // Wave wv handles wall segments s = wv, wv+W, ... and its neighbour chunk, for
 // all 8 rays; max is order-free, so the W partial maxima combine exactly.
 template <int LY, int C, class SH>
-__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, SH& S, float x, float y,
+__device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, const SH& S, float x, float y,
                                                   const float rdx[8], const float rdy[8], float prox[8],
-                                                  const uint32_t* disc_cand = nullptr, float cyw = 1.0f,
-                                                  float syw = 0.0f) {
+                                                  const uint32_t* disc_cand = nullptr) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     // wall segments: only those whose line passes within the 0.1 m ray length.
@@ -896,46 +804,10 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
         const uint32_t cand = disc_cand ? *disc_cand
                                         : chunk_mask<C>(L, S.xy, x, y,
                                                         [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
-#if SWARM_DISC_BITS
-        // the same hit tests per ray; only the rays THIS lane's disc passes the pre-test for are
-        // evaluated (the set bits of its own mask: <= 2 for a disc farther than 0.068 m, whose
-        // angular half-width is < 31 degrees against >= 32-degree ray gaps), the readings maxed into
-        // this lane's LDS slots (a reading is a non-negative float: its bits order as unsigned).
-        // The ray direction of bit k is re-evaluated with observe()'s expression: bitwise rdx[k], rdy[k].
-#pragma unroll
-        for (int k = 0; k < 8; ++k) S.dmax[k][L.tid] = 0u;
-        for_each_cand(L, S.xy, cand, [&](int, float2 p) {
-            SWARM_WT(L.wt_disc++);
-            const float dx = p.x - x, dy = p.y - y;
-            const float dsq = dx * dx + dy * dy;
-            uint32_t m = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const float proj = rdx[k] * dx + rdy[k] * dy;
-                const float csq = dsq - proj * proj;
-                m |= ((proj > 0.0f) & (csq <= g.r2)) ? (1u << k) : 0u;
-            }
-            while (m) {
-                const int k = __builtin_ctz(m);
-                m &= m - 1u;
-                const float2 a = S.adir[k];
-                const float rx = a.x * cyw - a.y * syw, ry = a.x * syw + a.y * cyw;
-                const float proj = rx * dx + ry * dy;
-                const float csq = dsq - proj * proj;
-                const float hc = fsqrt(fmaxf(g.r2 - csq, 0.0f));
-                const float hd = fmaxf(proj - hc, 0.0f);
-                const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
-                if (hd <= g.prox_range) atomicMax(&S.dmax[k][L.tid], __float_as_uint(rv));
-            }
-        });
-#pragma unroll
-        for (int k = 0; k < 8; ++k) prox[k] = fmaxf(prox[k], __uint_as_float(S.dmax[k][L.tid]));
-#else
         for_each_cand(L, S.xy, cand, [&](int, float2 p) {
             SWARM_WT(L.wt_disc++);
             disc(p.x - x, p.y - y);
         });
-#endif
     } else {
         unsigned long long cand = 0;
 #pragma unroll
@@ -1385,7 +1257,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, flo
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
     } else {
-        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr, cyw, syw);
+        proximity_partial<LY, C>(g, L, S, x, y, rdx, rdy, prox, FUSE ? &mprox : nullptr);
     }
     SWARM_PH_NEXT(L, PH_PROX, wt_t);
     if (!(SWARM_ABLATE & 1))
@@ -1830,7 +1702,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;
     const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
-    __shared__ Shared<LY, 4, false> SO;   // observation: position tile, inside flags, partial slots, tables
+    __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
     __shared__ float yaw_tile[64];
     const int lane = threadIdx.x & 63;
     const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
