@@ -244,3 +244,17 @@ def test_attention_terms_concurrent_streams(gpu_device):
         torch.cuda.synchronize(gpu_device)
         for k in range(2):
             assert torch.equal(outs[k], alone[k])
+
+
+def test_input_flag_is_one_per_device(gpu_device):
+    """'cuda' and 'cuda:<current>' name the same input-check flag: a trainer built with
+    device='cuda' reads the flag the kernels set through tensors on cuda:0."""
+    from SwarmACB_isaac.agents._trainer import _bad_action_flag, _flag_key, check_policy_inputs
+
+    with torch.cuda.device(gpu_device):
+        assert _flag_key("cuda") == _flag_key(gpu_device) == f"cuda:{torch.cuda.current_device()}"
+        assert _bad_action_flag("cuda") is _bad_action_flag(gpu_device)
+        _bad_action_flag(gpu_device).fill_(4)
+        with pytest.raises(ValueError):
+            check_policy_inputs("cuda")
+        check_policy_inputs(gpu_device)                                   # cleared by the first check
