@@ -1714,16 +1714,12 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // Waves per SIMD the layout-203 register budget must allow: 5 (96 VGPRs, no spill). The natural
 // allocation (100 VGPRs) held 4; the fifth resident wave is what a decision split into env groups
 // on streams (swarm_step_streams) fills the SIMDs with: C2 with 2 groups 8.15 -> 9.12e9
-// agent-steps/s; 6 waves (80 VGPRs, 52 B of scratch) 8.6e9.
+// agent-steps/s; 6 waves (80 VGPRs, 52 B of scratch) 8.6e9. Measured and not kept:
+// the range-and-bearing half of the observation moved onto the physics wave to even out the two
+// chains (bitwise, parity green): 53.0-55.2 vs 44.9 us per decision at 5-7 waves per SIMD with
+// 2 groups, 75 vs 62 us with one group at 6 or 8 waves (profiles/r06/variants/sweep_s8_pipe_rab.jsonl).
 #ifndef SWARM_PIPE_MIN_WAVES
 #define SWARM_PIPE_MIN_WAVES 5
-#endif
-// SWARM_PIPE_RAB=1: the range-and-bearing half of each substep's observation runs on the physics
-// wave (after its contact solver), the observation wave keeps proximity and light, so the two
-// waves' per-substep chains are closer in length (layout 103's phases: physics ~27 %, proximity
-// ~29 %, range-and-bearing ~23 %).
-#ifndef SWARM_PIPE_RAB
-#define SWARM_PIPE_RAB 0
 #endif
 template <int MISSION>
 __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
@@ -1731,13 +1727,8 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     uint64_t reset_any) {
     constexpr int PROFILE = ISAAC, LY = 103, NA = 20, C = 7;
     const Geom& g = kGeomTab[MISSION][PROFILE];
-#if SWARM_PIPE_RAB
-    __shared__ Shared<LY, 4> SP;   // physics: push tile, exchange slots (contact sums, range-and-bearing), tables
-    __shared__ Shared<LY, 2> SO;   // observation: position tile, proximity maxima slots, tables
-#else
     __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
     __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
-#endif
     __shared__ float yaw_tile[64];
     const int lane = threadIdx.x & 63;
     const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
@@ -1772,9 +1763,6 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
         }
         float rew_acc = 0.0f;
         bool trunc_acc = false;
-        float rab_ax = 0.0f, rab_ay = 0.0f;   // SWARM_PIPE_RAB: the attraction sums of the last substep
-        (void)rab_ax;
-        (void)rab_ay;
         const DevReplay rp{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
         for (int s = 0; s < n_sub; ++s) {
             const uint64_t tick = tick0 + (uint64_t)s;
@@ -1816,37 +1804,6 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
                 if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
             }
             trunc_acc |= tout;
-#if SWARM_PIPE_RAB
-            // the range-and-bearing half of substep s's observation on this wave (observe()'s
-            // expressions: publish, the exact range mask, the chunk's Philox block, the partial sums
-            // combined in part order, ztilde and the projections), written as the observation row's
-            // chunks 4 (ground, ztilde) and 5 (projections); the observation wave does the rest
-            {
-                publish<LY>(g, L, SP, x, y);
-                float syw, cyw;
-                sincosf(yaw, &syw, &cyw);
-                const uint32_t mrab = chunk_mask<C>(L, SP.xy, x, y,
-                                                    [&](float dx, float dy) { return dx * dx + dy * dy < g.rab_pre_lim; });
-                const uint4 rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
-                float n, wx, wy;
-                rab_partial<C>(g, L, SP.xy, SP.ins, x, y, cyw, syw, nullptr, RNG_RAB_OBS, tick, n, wx, wy, rab_ax, rab_ay,
-                               &mrab, &rb, SP.seg);
-                combine<LY, C>(L, SP, false, nullptr, n, wx, wy, rab_ax, rab_ay);
-                float zt, r4[4];
-                rab_finish(g, n, wx, wy, zt, r4, SP.zt);
-                if (L.valid && out.obs) {
-                    const float gv = 0.5f * (float)ground_code<MISSION, PROFILE>(g, x, y);
-                    float* o = out.obs + ((uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i) * (uint32_t)L.obs_dim;
-                    if (L.obs_dim == 24) {
-                        float4* o4 = reinterpret_cast<float4*>(o);
-                        if (L.p == 1) o4[4] = make_float4(gv, gv, gv, zt);        // chunk c by part c % 3
-                        if (L.p == 2) o4[5] = make_float4(r4[0], r4[1], r4[2], r4[3]);
-                    } else if (L.p == 0) {
-                        *reinterpret_cast<float4*>(o) = make_float4(gv, gv, gv, zt);
-                    }
-                }
-            }
-#endif
             __syncthreads();                   // A_s: the observation wave is done with substep s - 1
             if (L.p == 0) {
                 SO.xy[L.r] = make_float2(x, y);
@@ -1863,11 +1820,6 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             st.wr[q] = wr;
             st.gprev[q] = (uint8_t)gprev;
             st.flags[q] = (uint8_t)flags;
-#if SWARM_PIPE_RAB
-            const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
-            st.cache[4 * EN + q] = rab_ax;   // the attraction vector of the last substep (DG:114)
-            st.cache[5 * EN + q] = rab_ay;
-#endif
             if (L.i == 0) {
                 st.ep_len[L.env] = ep_len;
                 st.ep_rew[L.env] = ep_rew;
@@ -1887,47 +1839,17 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             __syncthreads();                   // B_s
             const float2 p = SO.xy[L.r];
             const float yaw = yaw_tile[L.r];
-#if SWARM_PIPE_RAB
-            // the proximity and light half of observe() (the physics wave wrote chunks 4-5)
-            const bool need_agg = s == n_sub - 1;
-            publish<LY>(g, L, SO, p.x, p.y);
-            float syw, cyw;
-            sincosf(yaw, &syw, &cyw);
-            float rdx[8], rdy[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                rdx[k] = g.cos_a[k] * cyw - g.sin_a[k] * syw;
-                rdy[k] = g.cos_a[k] * syw + g.sin_a[k] * cyw;
-            }
-            float prox[8], lt[8];
-            const uint32_t mprox = chunk_mask<C>(L, SO.xy, p.x, p.y,
-                                                 [](float dx, float dy) { return dx * dx + dy * dy <= 0.0200f; });
-            proximity_partial<LY, C>(g, L, SO, p.x, p.y, rdx, rdy, prox, &mprox);
-            combine_prox<LY>(L, SO, prox);
-            if (need_agg) proximity_aggregate(g, prox, cache.pv, cache.pa);
-            light<MISSION>(g, p.x, p.y, cyw, syw, lt, cache.lv, cache.la, need_agg);
-            if (L.valid && out.obs && L.obs_dim == 24) {
-                float4* o4 = reinterpret_cast<float4*>(out.obs + ((uint32_t)L.env * (uint32_t)L.N + (uint32_t)L.i) * 24u);
-                if (L.p == 0) o4[0] = make_float4(prox[0], prox[1], prox[2], prox[3]);
-                if (L.p == 1) o4[1] = make_float4(prox[4], prox[5], prox[6], prox[7]);
-                if (L.p == 2) o4[2] = make_float4(lt[0], lt[1], lt[2], lt[3]);
-                if (L.p == 0) o4[3] = make_float4(lt[4], lt[5], lt[6], lt[7]);
-            }
-#else
             float syaw, cyaw;
             observe<MISSION, PROFILE, LY, C>(g, L, SO, p.x, p.y, yaw, nullptr, tick0 + (uint64_t)s, out.obs, cache, syaw,
                                              cyaw, s == n_sub - 1);
-#endif
         }
         if (L.valid && L.p == 0) {
             st.cache[q] = cache.pv;
             st.cache[EN + q] = cache.pa;
             st.cache[2 * EN + q] = cache.lv;
             st.cache[3 * EN + q] = cache.la;
-#if !SWARM_PIPE_RAB
             st.cache[4 * EN + q] = cache.ax;
             st.cache[5 * EN + q] = cache.ay;
-#endif
         }
     }
 }
