@@ -1718,6 +1718,10 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // the range-and-bearing half of the observation moved onto the physics wave to even out the two
 // chains (bitwise, parity green): 53.0-55.2 vs 44.9 us per decision at 5-7 waves per SIMD with
 // 2 groups, 75 vs 62 us with one group at 6 or 8 waves (profiles/r06/variants/sweep_s8_pipe_rab.jsonl).
+// Also measured and not kept: heaviest-first dispatch (each launch wrote the next launch's block ->
+// arena order, arenas with >= t moving solver iterations in front, one atomic per arena; bitwise
+// equal): 50-56 vs 45.5-46.6 us per decision for t = 6 / 10 / 14 at 2-3 groups - a permuted order
+// loses more than the tail it shortens (profiles/r06/order/).
 #ifndef SWARM_PIPE_MIN_WAVES
 #define SWARM_PIPE_MIN_WAVES 5
 #endif

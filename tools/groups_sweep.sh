@@ -3,13 +3,16 @@
 # no per-decision join) at the C2 workload, alternating K, layouts and (optionally) variant
 # libraries over REPS passes on one box, default and driver (--steps 20 --warmup 5) arguments.
 #   OUT=gpurun_out/x REPS=2 KS="1 2 3" LAYOUTS="0 203" VLIBS="build/variants/lib_a.so ..." tools/groups_sweep.sh
+# ORDERS="0 6 10" also alternates the layout-203 dispatch order (SWARM_ARENA_ORDER: heavy threshold, 0 = identity).
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/groups}
 mkdir -p $OUT
 for rep in $(seq 1 ${REPS:-2}); do
+  for ord in ${ORDERS:-lib}; do
   for lib in ${VLIBS:-product}; do
     lname=$(basename $lib .so); lname=${lname#lib_}
+    if [ "$ord" = lib ]; then unset SWARM_ARENA_ORDER; else export SWARM_ARENA_ORDER=$ord; lname=${lname}_o$ord; fi
     for ly in ${LAYOUTS:-0}; do
       for k in ${KS:-1 2 3}; do
         for args in "" "--steps 20 --warmup 5"; do
@@ -25,9 +28,11 @@ for rep in $(seq 1 ${REPS:-2}); do
 import json, sys
 d = json.loads(sys.stdin.read()); r = d['roofline']
 print(json.dumps({'rep': $rep, 'tag': '$tag', 'value': d['value'], 'decision_us': r['kernel_avg_us'],
-                  'layout': r['layout'], 'groups': r['groups'], 'ms_per_step': d['ms_per_step']}))" | tee -a $OUT/sweep.jsonl
+                  'layout': r['layout'], 'groups': r['groups'], 'ms_per_step': d['ms_per_step'],
+                  'order': '$ord'}))" | tee -a $OUT/sweep.jsonl
         done
       done
     done
+  done
   done
 done
