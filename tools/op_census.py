@@ -26,6 +26,7 @@ class Census(TorchDispatchMode):
         super().__init__()
         self.ops = ops
         self.count = collections.Counter()
+        self.bytes = collections.Counter()   # bytes written by the op (its tensor outputs)
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func.overloadpacket.__name__
@@ -40,6 +41,10 @@ class Census(TorchDispatchMode):
                 if node is not None:
                     site = f"<backward> {node.name()}"
             self.count[(name, site)] += 1
+            out = func(*args, **(kwargs or {}))
+            outs = out if isinstance(out, (tuple, list)) else (out,)
+            self.bytes[(name, site)] += sum(t.numel() * t.element_size() for t in outs if isinstance(t, torch.Tensor))
+            return out
         return func(*args, **(kwargs or {}))
 
 
@@ -90,6 +95,9 @@ def main():
     print("\nby source line:")
     for (name, site), n in c.count.most_common(a.top):
         print(f"  {n / a.steps:8.1f}  {name:28s} {site}")
+    print("\nby bytes written per step (MB; a bandwidth proxy of the glue ops):")
+    for (name, site), b in c.bytes.most_common(a.top):
+        print(f"  {b / a.steps / 1e6:9.2f} MB  {c.count[(name, site)] / a.steps:6.1f} calls  {name:24s} {site}")
 
 
 if __name__ == "__main__":
