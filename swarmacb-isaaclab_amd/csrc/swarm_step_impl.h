@@ -1722,6 +1722,10 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // arena order, arenas with >= t moving solver iterations in front, one atomic per arena; bitwise
 // equal): 50-56 vs 45.5-46.6 us per decision for t = 6 / 10 / 14 at 2-3 groups - a permuted order
 // loses more than the tail it shortens (profiles/r06/order/).
+// And 6 waves per SIMD with the proximity rays serialised through the scheduler (one sched_barrier
+// per ray: the observation role alone then fits 80 VGPRs without spills, physics 67, but the joint
+// kernel still spills 14): 47.3-47.6 vs 45.2-45.8 us per decision at 2 groups, equal at 3
+// (profiles/r06/variants/sweep_s14_prox_serial_6waves.jsonl).
 #ifndef SWARM_PIPE_MIN_WAVES
 #define SWARM_PIPE_MIN_WAVES 5
 #endif
