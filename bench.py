@@ -513,6 +513,10 @@ def main():
     first = starts[0]
     region_s = (max(first.elapsed_time(e) for e in ends) - min(first.elapsed_time(e) for e in starts)) / 1e3
     avg_kernel_s = region_s / n_dec
+    # per stream: its back-to-back launches' region / decisions = the average duration of one of its
+    # launches (what rocprofv3 --stats reports per launch; with groups > 1 the streams' launches
+    # overlap, so this exceeds the per-decision share avg_kernel_s of the region)
+    stream_launch_us = [s_.elapsed_time(e_) * 1e3 / n_dec for s_, e_ in zip(starts, ends)]
     if gate_timed_out or elapsed < 0.98 * region_s:
         print(f"bench.py: rank {rank}: invalid timed region (gate timed out: {gate_timed_out}; wall "
               f"{elapsed * 1e3:.3f} ms vs GPU events {region_s * 1e3:.3f} ms): rerun with fewer --steps",
@@ -534,6 +538,7 @@ def main():
         traffic = pmc.get("hbm_bytes_per_decision", pmc.get("hbm_bytes_per_launch"))
         roofline = valu_roofline(pmc, pmc_why, avg_kernel_s, achieved, traffic, E, dp, bytes_per_launch,
                                  lib_sha256(lib_path) if lib_path else None, eng.split_layout(args.groups), args.groups)
+        roofline["launch_avg_us_per_stream"] = stream_launch_us
         line = {
             "metric": METRIC,
             "value": value,

@@ -1726,6 +1726,9 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 // per ray: the observation role alone then fits 80 VGPRs without spills, physics 67, but the joint
 // kernel still spills 14): 47.3-47.6 vs 45.2-45.8 us per decision at 2 groups, equal at 3
 // (profiles/r06/variants/sweep_s14_prox_serial_6waves.jsonl).
+// Wave priority in this layout (the physics wave's graded bumps; mirrored onto the observation wave
+// at every hand-over; or none at all): 45.0-45.8 us per decision all three, within the noise
+// (profiles/r06/variants/sweep_s16_pipe_priority.jsonl): the bumps stay, as in layout 103.
 #ifndef SWARM_PIPE_MIN_WAVES
 #define SWARM_PIPE_MIN_WAVES 5
 #endif
