@@ -18,6 +18,18 @@ template void launch_reset_m<SWARM_MISSION_ID>(const Geom&, const DevState&, con
 extern "C" int swarm_debug_wave_log(void* host, size_t bytes) { return swarm::read_wave_log(host, bytes); }
 #endif
 
+#if SWARM_PIPE_DIAG && SWARM_MISSION_ID == 2
+// diagnostic builds only (tools/pipe_diag.py): layout 203's per-role clocks; reset = zero them
+extern "C" int swarm_debug_pipe_diag(unsigned long long* host, int reset) {
+    if (reset) {
+        static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(swarm::g_pipe_diag), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(swarm::g_pipe_diag), 8 * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #if SWARM_ARENA_PERM && SWARM_MISSION_ID == 2
 // experiment builds only (tools/arena_balance.py): the block -> arena permutation of the Homing
 // step kernel, and the per-arena costs / per-block hardware slots of its last launch

@@ -1732,6 +1732,32 @@ __global__ __launch_bounds__(64 * ly_waves(LY), SWARM_MIN_WAVES_PER_SIMD) void s
 #ifndef SWARM_PIPE_MIN_WAVES
 #define SWARM_PIPE_MIN_WAVES 5
 #endif
+// SWARM_PIPE_DIAG=1 (diagnostic build, tools/pipe_diag.py): every wave of layout 203 adds its shader
+// clocks alive and spent at the two hand-over barriers per substep to g_pipe_diag (physics: [0] alive,
+// [1] at barriers, [2] waves; observation: [3], [4], [5]).
+#ifndef SWARM_PIPE_DIAG
+#define SWARM_PIPE_DIAG 0
+#endif
+#if SWARM_PIPE_DIAG
+static __device__ unsigned long long g_pipe_diag[8];
+#define SWARM_PD_BEGIN() const uint64_t pd_t0 = __builtin_amdgcn_s_memtime(); uint64_t pd_wait = 0, pd_ta = 0
+#define SWARM_PD_BAR0() pd_ta = __builtin_amdgcn_s_memtime()
+#define SWARM_PD_BAR1() pd_wait += __builtin_amdgcn_s_memtime() - pd_ta
+#define SWARM_PD_END(k)                                                                          \
+    do {                                                                                         \
+        const uint64_t pd_tot = __builtin_amdgcn_s_memtime() - pd_t0;                            \
+        if (lane == 0) {                                                                         \
+            atomicAdd(&g_pipe_diag[3 * (k)], (unsigned long long)pd_tot);                        \
+            atomicAdd(&g_pipe_diag[3 * (k) + 1], (unsigned long long)pd_wait);                   \
+            atomicAdd(&g_pipe_diag[3 * (k) + 2], 1ull);                                          \
+        }                                                                                        \
+    } while (0)
+#else
+#define SWARM_PD_BEGIN() ((void)0)
+#define SWARM_PD_BAR0() ((void)0)
+#define SWARM_PD_BAR1() ((void)0)
+#define SWARM_PD_END(k) ((void)0)
+#endif
 template <int MISSION>
 __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     const Geom gr, const DevState st, const void* __restrict__ actions, const DevOut out, uint64_t tick0, int n_sub,
@@ -1775,6 +1801,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
         float rew_acc = 0.0f;
         bool trunc_acc = false;
         const DevReplay rp{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+        SWARM_PD_BEGIN();
         for (int s = 0; s < n_sub; ++s) {
             const uint64_t tick = tick0 + (uint64_t)s;
             const float lw = clampf(ax, -1.0f, 1.0f) * g.max_speed;                   // DG:807-809
@@ -1815,13 +1842,16 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
                 if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
             }
             trunc_acc |= tout;
+            SWARM_PD_BAR0();
             __syncthreads();                   // A_s: the observation wave is done with substep s - 1
             if (L.p == 0) {
                 SO.xy[L.r] = make_float2(x, y);
                 yaw_tile[L.r] = yaw;
             }
             __syncthreads();                   // B_s: the tile of substep s is written
+            SWARM_PD_BAR1();
         }
+        SWARM_PD_END(0);
         if (L.valid && L.p == 0) {
             st.x[q] = x;
             st.y[q] = y;
@@ -1845,9 +1875,12 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
         const uint32_t EN = (uint32_t)L.E * (uint32_t)L.N;
         stage_tables<LY>(g, SO, lane);
         Agg cache = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        SWARM_PD_BEGIN();
         for (int s = 0; s < n_sub; ++s) {
+            SWARM_PD_BAR0();
             __syncthreads();                   // A_s
             __syncthreads();                   // B_s
+            SWARM_PD_BAR1();
             const float2 p = SO.xy[L.r];
             const float yaw = yaw_tile[L.r];
             float syaw, cyaw;
@@ -1862,6 +1895,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             st.cache[4 * EN + q] = cache.ax;
             st.cache[5 * EN + q] = cache.ay;
         }
+        SWARM_PD_END(1);
     }
 }
 
