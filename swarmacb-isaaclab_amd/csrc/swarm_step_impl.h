@@ -1254,14 +1254,15 @@ __device__ __forceinline__ void combine_prox(const Lane& L, SH& S, float prox[8]
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-template <int MISSION, int PROFILE, int LY, int C, class SH>
+// SC_GIVEN: (syw, cyw) already hold sin / cos of yaw (layout 203's physics wave hands them over)
+template <int MISSION, int PROFILE, int LY, int C, bool SC_GIVEN = false, class SH>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw, bool need_agg = true) {
     SWARM_PH_T(wt_t);
     publish<LY>(g, L, S, x, y);
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
-    sincosf(yaw, &syw, &cyw);
+    if constexpr (!SC_GIVEN) sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -1766,7 +1767,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     const Geom& g = kGeomTab[MISSION][PROFILE];
     __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
     __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
-    __shared__ float yaw_tile[64];
+    __shared__ float2 sc_tile[64];        // sin / cos of each robot's yaw, handed over with the positions
     const int lane = threadIdx.x & 63;
     const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
     // each role builds its own lane context (separate live ranges for the two register budgets)
@@ -1802,14 +1803,17 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
         bool trunc_acc = false;
         const DevReplay rp{nullptr, nullptr, nullptr, nullptr, 0, nullptr};
         SWARM_PD_BEGIN();
+        // sin / cos of the current yaw: evaluated once per substep, at its end, for the next
+        // substep's drive AND the observation wave's rays (handed over in sc_tile), as layout 103
+        // carries them from its observation pass
+        float syaw, cyaw;
+        sincosf(yaw, &syaw, &cyaw);
         for (int s = 0; s < n_sub; ++s) {
             const uint64_t tick = tick0 + (uint64_t)s;
             const float lw = clampf(ax, -1.0f, 1.0f) * g.max_speed;                   // DG:807-809
             const float rw = clampf(ay, -1.0f, 1.0f) * g.max_speed;
             wl = lw;
             wr = rw;
-            float syaw, cyaw;
-            sincosf(yaw, &syaw, &cyaw);   // layout 103 carries these from the observation of yaw
             for (int d = 0; d < gr.decimation; ++d) {
                 const float qx = x, qy = y;
                 if (d > 0) sincosf(yaw, &syaw, &cyaw);
@@ -1842,11 +1846,12 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
                 if constexpr (MISSION == FORAGING) flags = (y <= g.z_nest_top) ? 2 : 0;
             }
             trunc_acc |= tout;
+            sincosf(yaw, &syaw, &cyaw);
             SWARM_PD_BAR0();
             __syncthreads();                   // A_s: the observation wave is done with substep s - 1
             if (L.p == 0) {
                 SO.xy[L.r] = make_float2(x, y);
-                yaw_tile[L.r] = yaw;
+                sc_tile[L.r] = make_float2(syaw, cyaw);
             }
             __syncthreads();                   // B_s: the tile of substep s is written
             SWARM_PD_BAR1();
@@ -1882,10 +1887,10 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             __syncthreads();                   // B_s
             SWARM_PD_BAR1();
             const float2 p = SO.xy[L.r];
-            const float yaw = yaw_tile[L.r];
-            float syaw, cyaw;
-            observe<MISSION, PROFILE, LY, C>(g, L, SO, p.x, p.y, yaw, nullptr, tick0 + (uint64_t)s, out.obs, cache, syaw,
-                                             cyaw, s == n_sub - 1);
+            const float2 sc = sc_tile[L.r];
+            float syaw = sc.x, cyaw = sc.y;
+            observe<MISSION, PROFILE, LY, C, true>(g, L, SO, p.x, p.y, 0.0f, nullptr, tick0 + (uint64_t)s, out.obs, cache,
+                                                   syaw, cyaw, s == n_sub - 1);
         }
         if (L.valid && L.p == 0) {
             st.cache[q] = cache.pv;
