@@ -1157,17 +1157,23 @@ __device__ __forceinline__ void critic5(const Geom& g, float x, float y, float y
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
 // Publishes positions + "strictly inside the arena" flags (LOS shortcut).
-template <int LY, class SH>
-__device__ __forceinline__ void publish(const Geom& g, const Lane& L, SH& S, float x, float y) {
+// "strictly inside the arena" (every face > 1e-3 away): |p| < apothem - 1e-3 - margin implies it,
+// so only waves with a robot outside that radius test the faces (the value is the same either way);
+// the flag only selects a shortcut (a robot flagged "not inside" gets the full, exact line-of-sight
+// test), so the conservative radius keeps results exact
+__device__ __forceinline__ bool inside_flag(const Geom& g, float x, float y) {
     bool ins = true;
-    // |p| < apothem - 1e-3 - margin implies every face is > 1e-3 away; the flag
-    // only selects a shortcut (a robot flagged "not inside" gets the full,
-    // exact line-of-sight test), so the conservative radius keeps results exact
     if (__any(fmaf(x, x, y * y) >= g.ins_safe_r2)) {
 #pragma unroll
         for (int k = 0; k < 12; ++k)
             ins &= (x - g.face_px[k]) * g.face_nx[k] + (y - g.face_py[k]) * g.face_ny[k] > 1e-3f;
     }
+    return ins;
+}
+
+template <int LY, class SH>
+__device__ __forceinline__ void publish(const Geom& g, const Lane& L, SH& S, float x, float y) {
+    const bool ins = inside_flag(g, x, y);
     if (L.p == 0) {
         S.xy[L.r] = make_float2(x, y);
         S.ins[L.r] = ins ? 1 : 0;
@@ -1254,13 +1260,15 @@ __device__ __forceinline__ void combine_prox(const Lane& L, SH& S, float prox[8]
 // ---------------------------------------------------------------------------
 //  Observation pass (writes obs + returns the aggregates for the cache)
 // ---------------------------------------------------------------------------
-// SC_GIVEN: (syw, cyw) already hold sin / cos of yaw (layout 203's physics wave hands them over)
-template <int MISSION, int PROFILE, int LY, int C, bool SC_GIVEN = false, class SH>
+// SC_GIVEN: (syw, cyw) already hold sin / cos of yaw (layout 203's physics wave hands them over).
+// PUB_GIVEN: S.xy / S.ins already hold this substep's positions and inside flags (layout 203's
+// physics wave writes them with the hand-over): no publish.
+template <int MISSION, int PROFILE, int LY, int C, bool SC_GIVEN = false, bool PUB_GIVEN = false, class SH>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
                                         float& cyw, bool need_agg = true) {
     SWARM_PH_T(wt_t);
-    publish<LY>(g, L, S, x, y);
+    if constexpr (!PUB_GIVEN) publish<LY>(g, L, S, x, y);
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
     if constexpr (!SC_GIVEN) sincosf(yaw, &syw, &cyw);
     float rdx[8], rdy[8];
@@ -1847,10 +1855,15 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             }
             trunc_acc |= tout;
             sincosf(yaw, &syaw, &cyaw);
+            // the observation's "strictly inside" flags too (publish() for the observation wave, which
+            // only reads the tile): 44.6-45.1 -> 44.1-44.6 us per decision (profiles/r06/variants/
+            // sweep_s23_handover.jsonl; handing over the 8 ray directions through LDS as well: slower)
+            const bool ins_f = inside_flag(g, x, y);
             SWARM_PD_BAR0();
             __syncthreads();                   // A_s: the observation wave is done with substep s - 1
             if (L.p == 0) {
                 SO.xy[L.r] = make_float2(x, y);
+                SO.ins[L.r] = ins_f ? 1 : 0;
                 sc_tile[L.r] = make_float2(syaw, cyaw);
             }
             __syncthreads();                   // B_s: the tile of substep s is written
@@ -1889,8 +1902,8 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             const float2 p = SO.xy[L.r];
             const float2 sc = sc_tile[L.r];
             float syaw = sc.x, cyaw = sc.y;
-            observe<MISSION, PROFILE, LY, C, true>(g, L, SO, p.x, p.y, 0.0f, nullptr, tick0 + (uint64_t)s, out.obs, cache,
-                                                   syaw, cyaw, s == n_sub - 1);
+            observe<MISSION, PROFILE, LY, C, true, true>(g, L, SO, p.x, p.y, 0.0f, nullptr, tick0 + (uint64_t)s, out.obs,
+                                                         cache, syaw, cyaw, s == n_sub - 1);
         }
         if (L.valid && L.p == 0) {
             st.cache[q] = cache.pv;
