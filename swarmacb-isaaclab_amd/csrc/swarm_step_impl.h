@@ -1263,10 +1263,12 @@ __device__ __forceinline__ void combine_prox(const Lane& L, SH& S, float prox[8]
 // SC_GIVEN: (syw, cyw) already hold sin / cos of yaw (layout 203's physics wave hands them over).
 // PUB_GIVEN: S.xy / S.ins already hold this substep's positions and inside flags (layout 203's
 // physics wave writes them with the hand-over): no publish.
+// rb_given: this part's packet-loss Philox block of the substep, drawn by layout 203's physics wave
+// (the same rng4 call: it depends on no position).
 template <int MISSION, int PROFILE, int LY, int C, bool SC_GIVEN = false, bool PUB_GIVEN = false, class SH>
 __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, float x, float y, float yaw,
                                         const float* u_replay, uint64_t tick, float* obs, Agg& agg, float& syw,
-                                        float& cyw, bool need_agg = true) {
+                                        float& cyw, bool need_agg = true, const uint4* rb_given = nullptr) {
     SWARM_PH_T(wt_t);
     if constexpr (!PUB_GIVEN) publish<LY>(g, L, S, x, y);
     SWARM_PH_NEXT(L, PH_PUBLISH, wt_t);
@@ -1284,7 +1286,7 @@ __device__ __forceinline__ void observe(const Geom& g, const Lane& L, SH& S, flo
     uint4 rb = make_uint4(0, 0, 0, 0);
     if constexpr (FUSE) {
         obs_masks<C>(g, L, S.xy, x, y, mprox, mrab);
-        if (!u_replay) rb = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+        if (!u_replay) rb = rb_given ? *rb_given : rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
     }
     if (SWARM_ABLATE & 2) {
         for (int k = 0; k < 8; ++k) prox[k] = 0.0f;
@@ -1776,6 +1778,7 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
     __shared__ Shared<LY, 1> SP;   // physics: push tile, exchange slot, wall tables
     __shared__ Shared<LY, 4> SO;   // observation: position tile, inside flags, partial slots, tables
     __shared__ float2 sc_tile[64];        // sin / cos of each robot's yaw, handed over with the positions
+    __shared__ uint4 rb_tile[64];         // each lane's packet-loss Philox block of the substep
     const int lane = threadIdx.x & 63;
     const bool obs_wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) != 0;
     // each role builds its own lane context (separate live ranges for the two register budgets)
@@ -1866,6 +1869,10 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
                 SO.ins[L.r] = ins_f ? 1 : 0;
                 sc_tile[L.r] = make_float2(syaw, cyaw);
             }
+            // and each lane's packet-loss Philox block of the substep (position-free; the observation
+            // wave's ten dependent Philox rounds leave its chain: 92 instead of 96 VGPRs, 44.1-44.4 vs
+            // 44.2-44.7 us per decision, profiles/r06/variants/sweep_s24_philox_handover.jsonl)
+            rb_tile[lane] = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
             __syncthreads();                   // B_s: the tile of substep s is written
             SWARM_PD_BAR1();
         }
@@ -1902,8 +1909,9 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             const float2 p = SO.xy[L.r];
             const float2 sc = sc_tile[L.r];
             float syaw = sc.x, cyaw = sc.y;
+            const uint4 rbv = rb_tile[lane];
             observe<MISSION, PROFILE, LY, C, true, true>(g, L, SO, p.x, p.y, 0.0f, nullptr, tick0 + (uint64_t)s, out.obs,
-                                                         cache, syaw, cyaw, s == n_sub - 1);
+                                                         cache, syaw, cyaw, s == n_sub - 1, &rbv);
         }
         if (L.valid && L.p == 0) {
             st.cache[q] = cache.pv;
