@@ -1873,6 +1873,9 @@ __global__ __launch_bounds__(128, SWARM_PIPE_MIN_WAVES) void step_kernel_pipe(
             // wave's ten dependent Philox rounds leave its chain: 92 instead of 96 VGPRs, 44.1-44.4 vs
             // 44.2-44.7 us per decision, profiles/r06/variants/sweep_s24_philox_handover.jsonl)
             rb_tile[lane] = rng4(L, (uint32_t)L.i, ChunkRng<C>::block(L.p, 0), RNG_RAB_OBS, tick);
+            // (measured and not kept: the wall-segment proximity rays, which need only the robot's own
+            // pose, evaluated here and handed over: 45.4-45.7 vs 43.7-44.2 us per decision - the
+            // hand-over is then late, profiles/r06/variants/sweep_s25_wallrays_on_physics.jsonl)
             __syncthreads();                   // B_s: the tile of substep s is written
             SWARM_PD_BAR1();
         }
