@@ -29,6 +29,7 @@ import json, sys
 d = json.loads(sys.stdin.read()); r = d['roofline']
 print(json.dumps({'rep': $rep, 'tag': '$tag', 'value': d['value'], 'decision_us': r['kernel_avg_us'],
                   'layout': r['layout'], 'groups': r['groups'], 'ms_per_step': d['ms_per_step'],
+                  'stream_launch_us': r.get('launch_avg_us_per_stream'),
                   'order': '$ord'}))" | tee -a $OUT/sweep.jsonl
         done
       done
