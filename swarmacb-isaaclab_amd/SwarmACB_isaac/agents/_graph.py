@@ -19,6 +19,7 @@ update equals the eager one (tests/test_gpu_graph_step.py).
 
 from __future__ import annotations
 
+import gc
 import os
 import traceback
 import warnings
@@ -121,6 +122,11 @@ class GraphedStep:
         self.sig = sig
         self.graph = torch.cuda.CUDAGraph()
         ok = True
+        # no cyclic garbage collection inside the capture: an unreachable CUDAGraph of an earlier
+        # runner destroyed while a stream is capturing aborts the process (torch.cuda.graph collects
+        # once before it begins)
+        gc_on = gc.isenabled()
+        gc.disable()
         try:
             with torch.cuda.graph(self.graph):
                 self.out = self.fn(self.static)
@@ -128,6 +134,9 @@ class GraphedStep:
             where = "".join(traceback.format_exception(e)[-8:-1])
             warnings.warn(f"optimizer step not capturable, running eagerly: {e}\n{where}")
             ok = False
+        finally:
+            if gc_on:
+                gc.enable()
         # every rank takes the same path (captured collectives replayed on one rank and eager
         # ones on another would pair up wrongly and hang)
         if not all_ranks_agree(ok):

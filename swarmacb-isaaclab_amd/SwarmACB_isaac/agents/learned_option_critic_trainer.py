@@ -27,6 +27,7 @@ decision identical; agents/distributed.py).
 
 from __future__ import annotations
 
+import contextlib
 import copy
 import ctypes as C
 import math
@@ -549,6 +550,32 @@ class LearnedOptionCriticTrainer(TrainerBase):
             (self.option_critic, flat_states, encoded, focal_ids,
              {"joint": mem("option_joint_memory"), "baseline": mem("option_baseline_memory")}, L,
              ("joint", "baseline"))]
+        flat_returns = batch["returns"].reshape(-1)
+        flat_mask = loss_mask.reshape(-1)
+
+        def tr_loss(new, old_key):
+            return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,
+                                           denom=d_mask)
+
+        # The critics' passes and value losses share nothing with the actor's graph (no parameter,
+        # no gradient path: the critic values the actor's terms read are no-grad evaluations), so
+        # in a device step (_oc2_step, one process) they run on a side stream beside the actor's
+        # recurrences, and their backward and Adam step follow on it (_critic_side_stream).
+        side = self.__dict__.get("_critic_side")
+        critic_losses = None
+        if side is not None:
+            main = torch.cuda.current_stream(flat_states.device)
+            side.wait_stream(main)
+            # every tensor of this stream the side stream reads stays referenced until _oc2_step has
+            # joined the streams (no block of it is freed and reused here while the side stream may
+            # still read it; record_stream is not used: its deferred events break later captures)
+            self._side_keep = [flat_states, option_states, encoded, flat_joint_actions, focal_ids, flat_returns,
+                               flat_mask, batch, critic_requests]
+            with torch.cuda.stream(side):
+                ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes(critic_requests)
+                critic_losses = (tr_loss(new_team, "old_team_values"), tr_loss(new_action_bl, "old_action_baselines"),
+                                 tr_loss(new_joint, "old_joint_option_values"),
+                                 tr_loss(new_option_bl, "old_option_baselines"))
         # the actor's sequence pass and its next-state pass (termination logits at s' from the stored
         # post-decision memory, LOT:1140-1169) as two streams of one forward: their per-row layers run
         # once over both streams' rows, the recurrences per stream
@@ -572,7 +599,8 @@ class LearnedOptionCriticTrainer(TrainerBase):
         with torch.no_grad():
             ref_out = reference_actor.head_stage(r_ctx, opt_outs[1])
             ref_means, ref_stds = ref_out[3], ref_out[4]
-        ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes(critic_requests)
+        if side is None:
+            ((new_team,), (new_action_bl,), (new_joint, new_option_bl)), _ = batched_sequence_passes(critic_requests)
 
         # AOC: the manager is epsilon-soft over Q_Omega; no selector gradient (LOT:1050-1093)
         fused_opt = fused_option_terms(self.actor, option_values, options, loss_mask, boundary,
@@ -623,22 +651,19 @@ class LearnedOptionCriticTrainer(TrainerBase):
         next_option_values, next_term_logits = next_out[1][:, 0], next_out[2][:, 0]
         next_beta_logits = self.actor.selected_termination_logits(next_term_logits, options.reshape(-1)).view(B, L)
 
-        flat_returns = batch["returns"].reshape(-1)
-        flat_mask = loss_mask.reshape(-1)
         selected_local = option_values.gather(-1, options.unsqueeze(-1)).squeeze(-1).reshape(-1)
         local_option_value_mean = (selected_local * flat_mask).sum() / (
             n_mask_f if d_mask is not None else flat_mask.sum().clamp_min(1.0))
         option_value_spread = (option_values.std(dim=-1, unbiased=False) * loss_mask).sum() / n_mask
 
-        def tr_loss(new, old_key):
-            return trust_region_value_loss(new, batch[old_key].reshape(-1), flat_returns, current_eps, flat_mask,
-                                           denom=d_mask)
-
-        value_loss = tr_loss(new_team, "old_team_values")
         local_option_value_loss = tr_loss(selected_local, "old_local_option_values")
-        action_baseline_loss = tr_loss(new_action_bl, "old_action_baselines")
-        joint_option_value_loss = tr_loss(new_joint, "old_joint_option_values")
-        option_baseline_loss = tr_loss(new_option_bl, "old_option_baselines")
+        if critic_losses is not None:
+            value_loss, action_baseline_loss, joint_option_value_loss, option_baseline_loss = critic_losses
+        else:
+            value_loss = tr_loss(new_team, "old_team_values")
+            action_baseline_loss = tr_loss(new_action_bl, "old_action_baselines")
+            joint_option_value_loss = tr_loss(new_joint, "old_joint_option_values")
+            option_baseline_loss = tr_loss(new_option_bl, "old_option_baselines")
 
         # arrival-state termination theorem: peers keep their options, the focal robot
         # compares continuation with V_Omega over its counterfactual alternatives (LOT:1282-1317)
@@ -760,9 +785,10 @@ class LearnedOptionCriticTrainer(TrainerBase):
             # (separate products: the actor and critic losses are differentiated one after the other)
             na = len(actor)
             ta = torch.stack([losses[a].reshape(()) for _, a, _ in actor]) * staged[1][:na]
-            tc = torch.stack([losses[a].reshape(()) for a, _ in critic]) * staged[1][na:]
+            with self._critic_stream_ctx():
+                critic_loss = (torch.stack([losses[a].reshape(()) for a, _ in critic]) * staged[1][na:]).sum()
             terms = {name: ta[i] for i, (name, _, _) in enumerate(actor)}
-            return terms, ta.sum(), tc.sum()
+            return terms, ta.sum(), critic_loss
         terms = {
             "objective_intra_option": cfg.intra_option_coef * losses["intra_option_loss"],
             "objective_selector": cfg.selector_coef * losses["selector_loss"],
@@ -777,10 +803,29 @@ class LearnedOptionCriticTrainer(TrainerBase):
             "objective_termination_entropy": -cfg.termination_entropy_coef * losses["termination_entropy"],
         }
         actor_loss = sum(terms.values())
-        critic_loss = (cfg.value_coef * losses["value_loss"] + cfg.action_baseline_coef * losses["action_baseline_loss"]
-                       + cfg.option_value_coef * losses["joint_option_value_loss"]
-                       + cfg.option_baseline_coef * losses["option_baseline_loss"])
+        with self._critic_stream_ctx():
+            critic_loss = (cfg.value_coef * losses["value_loss"]
+                           + cfg.action_baseline_coef * losses["action_baseline_loss"]
+                           + cfg.option_value_coef * losses["joint_option_value_loss"]
+                           + cfg.option_baseline_coef * losses["option_baseline_loss"])
         return terms, actor_loss, critic_loss
+
+    def _critic_stream_ctx(self):
+        """The critic branch's stream context during a device step with a side stream (else a no-op)."""
+        side = self.__dict__.get("_critic_side")
+        return torch.cuda.stream(side) if side is not None else contextlib.nullcontext()
+
+    def _critic_side_stream(self):
+        """The side stream of the critics' branch in a device step, or None: one process only (the
+        critics' gradient all-reduce would otherwise share the communicator with the actor's from
+        another stream), CUDA, and SWARM_OC2_CRITIC_STREAM != 0."""
+        if (self.device.type != "cuda" or self.comm.active or self.critic_comm.active
+                or os.environ.get("SWARM_OC2_CRITIC_STREAM", "1") == "0"):
+            return None
+        st = self.__dict__.get("_critic_side_s")
+        if st is None:
+            st = self._critic_side_s = torch.cuda.Stream(self.device)
+        return st
 
     def _clip_step(self, kind: str, loss, comm, optimizer, params, max_norm: float, index: int):
         comm.zero_grad(optimizer)
@@ -890,8 +935,13 @@ class LearnedOptionCriticTrainer(TrainerBase):
         update. Accumulates into self._g (static tensors, so the step can be graphed)."""
         G, cfg = self._g, self.cfg
         G["samples"] += batch["loss_mask"].sum()
-        losses = self.compute_losses(batch, self.current_eps, self.reference_actor)
-        terms, actor_loss, critic_loss = self.objectives(losses)
+        side = self._critic_side_stream()
+        self._critic_side = side
+        try:
+            losses = self.compute_losses(batch, self.current_eps, self.reference_actor)
+            terms, actor_loss, critic_loss = self.objectives(losses)
+        finally:
+            self._critic_side = None
         kl = torch.stack([losses["action_approx_kl"].detach(), losses["option_approx_kl"].detach()]).double()
         policy_kl = torch.maximum(kl[0], kl[1])
         G["init_kl"].copy_(torch.where(G["nb"] == 0, policy_kl, G["init_kl"]))
@@ -900,7 +950,23 @@ class LearnedOptionCriticTrainer(TrainerBase):
         apply = ~G["stopped"] & ~over
         G["stopped"] |= over
         G["bad"][0] |= ~torch.isfinite(actor_loss.detach())
-        G["bad"][1] |= ~torch.isfinite(critic_loss.detach())
+        if side is None:
+            G["bad"][1] |= ~torch.isfinite(critic_loss.detach())
+        else:
+            # the critics' backward, clip and Adam step on their side stream, beside the actor's
+            # forward tail and step. The Adam step rewrites the option critic's parameters, which
+            # this stream's no-grad counterfactual pass (the termination advantage) reads: before
+            # it the side stream waits for everything this stream has enqueued so far (without
+            # that wait the step's result depended on the streams' timing)
+            main = torch.cuda.current_stream(self.device)
+            with torch.cuda.stream(side):
+                self.critic_comm.zero_grad(self.critic_optimizer)
+                critic_loss.backward()
+                self.critic_comm.all_reduce_grads()
+                norm_c = torch.nn.utils.clip_grad_norm_(self.critic_parameters, cfg.max_grad_norm,
+                                                        error_if_nonfinite=False)
+                side.wait_stream(main)
+                self.critic_optimizer.step()
         if self.device.type == "cuda":
             # save the actor's parameters + Adam state, take the step, and copy the saved
             # words back unless `apply` (one multi-tensor launch each way)
@@ -920,8 +986,16 @@ class LearnedOptionCriticTrainer(TrainerBase):
         G["grad_norms"][0] += torch.where(apply, norm_a.double(), torch.zeros_like(G["grad_norms"][0]))
         G["bad"][2] |= apply & ~torch.isfinite(norm_a)
         G["actor_updates"] += apply.double()
-        norm_c = self._clip_step_device(critic_loss, self.critic_comm, self.critic_optimizer,
-                                        self.critic_parameters, cfg.max_grad_norm)
+        if side is None:
+            norm_c = self._clip_step_device(critic_loss, self.critic_comm, self.critic_optimizer,
+                                            self.critic_parameters, cfg.max_grad_norm)
+        else:
+            # join: the side stream's results are read here; their blocks (the side stream's pool) are
+            # reused only by side-stream work of a later step, which waits for this stream at its fork
+            main = torch.cuda.current_stream(self.device)
+            main.wait_stream(side)
+            self._side_keep = None
+            G["bad"][1] |= ~torch.isfinite(critic_loss.detach())
         G["grad_norms"][1] += norm_c.double()
         G["bad"][3] |= ~torch.isfinite(norm_c)
         G["totals"] += _stack_f64([losses[n] for n in METRIC_NAMES] + [actor_loss, critic_loss]
