@@ -499,9 +499,31 @@ class TrainerBase:
             self._graph_warm = True
         return self._graphed
 
+    # whether the critic's branch runs on a side stream by default (SWARM_CRITIC_STREAM=0 / 1 overrides)
+    SIDE_STREAM_DEFAULT = False
+
+    def _side_stream(self):
+        """The side stream the critic's branch of an optimizer step runs on beside the actor's, or
+        None: CUDA, one process (a gradient all-reduce must not share the communicator across
+        streams) and SWARM_CRITIC_STREAM (default: the class's SIDE_STREAM_DEFAULT). The critic's
+        forward (passes, LSTM, value losses) is issued on it; autograd runs each backward op on its
+        forward op's stream, so one backward of the total loss overlaps the two branches, and the
+        engine joins the streams before optimizer.step()."""
+        env = os.environ.get("SWARM_CRITIC_STREAM")
+        on = self.SIDE_STREAM_DEFAULT if env is None else env != "0"
+        if self.device.type != "cuda" or self.comm.active or not on:
+            return None
+        st = self.__dict__.get("_side_s")
+        if st is None:
+            st = self._side_s = torch.cuda.Stream(self.device)
+        return st
+
     def optimizer_step(self, loss: torch.Tensor, step_index: int):
         self.comm.zero_grad(self.optimizer)
         loss.backward()
+        # the tensors of this stream the critic's side stream read stay referenced until the
+        # backward (whose end joins the streams) has been issued (_side_stream)
+        self._side_keep = None
         self.comm.all_reduce_grads()
         if self.grad_hook is not None:
             self.grad_hook(step_index, self.params)

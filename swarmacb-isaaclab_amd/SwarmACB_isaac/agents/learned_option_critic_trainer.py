@@ -818,9 +818,9 @@ class LearnedOptionCriticTrainer(TrainerBase):
     def _critic_side_stream(self):
         """The side stream of the critics' branch in a device step, or None: one process only (the
         critics' gradient all-reduce would otherwise share the communicator with the actor's from
-        another stream), CUDA, and SWARM_OC2_CRITIC_STREAM != 0."""
-        if (self.device.type != "cuda" or self.comm.active or self.critic_comm.active
-                or os.environ.get("SWARM_OC2_CRITIC_STREAM", "1") == "0"):
+        another stream), CUDA, and SWARM_OC2_CRITIC_STREAM (else SWARM_CRITIC_STREAM) != 0."""
+        env = os.environ.get("SWARM_OC2_CRITIC_STREAM", os.environ.get("SWARM_CRITIC_STREAM", "1"))
+        if self.device.type != "cuda" or self.comm.active or self.critic_comm.active or env == "0":
             return None
         st = self.__dict__.get("_critic_side_s")
         if st is None:

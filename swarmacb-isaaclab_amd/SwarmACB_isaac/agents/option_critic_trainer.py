@@ -48,6 +48,10 @@ _COLLECTOR_STATE = ("manager_memory_h", "manager_memory_c", "value_memory_h", "v
 class FixedOptionCriticTrainer(TrainerBase):
     """Learn decentralised option control from collective critic signals (OCT:99-959)."""
 
+    # the critic's passes on a side stream beside the manager's sequence: C4 optimizer step 2.82 ->
+    # 2.56 ms (profiles/r06/train/critic_stream/), graphed = eager bitwise
+    SIDE_STREAM_DEFAULT = True
+
     algo = "FixedOC"
     ckpt_prefix = "option_critic"
 
@@ -142,19 +146,38 @@ class FixedOptionCriticTrainer(TrainerBase):
         flat_option_ids = batch["critic_options"].reshape(B * L, N)
         critic_options = self._encode_options_for_critic(flat_option_ids)
         focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        # critic_pass, joint_action_pass and focal_baselines (OCT:571-608) as one batched pass
-        # (POCACritic.sequence_passes) whose memory shares the manager's LSTM launch
-        c_item, c_ctx = self.critic.sequence_passes_begin(
-            flat_states, critic_options, focal_ids,
-            {"value": mem("value_memory"), "joint": mem("joint_memory"), "baseline": mem("baseline_memory")},
-            sequence_length=L, passes=("value", "joint", "baseline"))
-        option_logits, c_out = self._manager_sequence(batch, c_item)
-        new_team_values, new_joint, new_baselines = self.critic.sequence_passes_end(c_out, c_ctx)
-        # PPO clip over the switch decisions (option_mask) inside the loss mask (OCT:515-525)
+        memories = {"value": mem("value_memory"), "joint": mem("joint_memory"), "baseline": mem("baseline_memory")}
+        flat_returns = batch["returns"].reshape(B * L)
+        flat_loss_mask = loss_mask.reshape(B * L)
         mask_flat = (batch["option_masks"].reshape(-1) > 0.5) & loss_mask.reshape(-1)
         nonterminal = 1.0 - dones
         term_mask = nonterminal * loss_mask
         d_pol, d_mask, d_term = self._denominators([mask_flat.sum(), loss_mask.sum(), term_mask.sum()])
+        side = self._side_stream()
+        if side is not None:
+            # the critic's three passes, their LSTM and value losses on the side stream, beside the
+            # manager's sequence (TrainerBase._side_stream); its inputs stay referenced until the
+            # backward has been issued
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            self._side_keep = [flat_states, critic_options, focal_ids, flat_returns, flat_loss_mask, batch, memories]
+            with torch.cuda.stream(side):
+                c_item, c_ctx = self.critic.sequence_passes_begin(flat_states, critic_options, focal_ids, memories,
+                                                                  sequence_length=L,
+                                                                  passes=("value", "joint", "baseline"))
+                c_out = lstm_sequences([c_item])[0][0] if c_item is not None else None
+                new_team_values, new_joint, new_baselines = self.critic.sequence_passes_end(c_out, c_ctx)
+                side_losses = self._value_losses(batch, new_team_values, new_joint, new_baselines, flat_returns,
+                                                 flat_loss_mask, current_eps, d_mask)
+            option_logits, _ = self._manager_sequence(batch)
+        else:
+            # critic_pass, joint_action_pass and focal_baselines (OCT:571-608) as one batched pass
+            # (POCACritic.sequence_passes) whose memory shares the manager's LSTM launch
+            c_item, c_ctx = self.critic.sequence_passes_begin(flat_states, critic_options, focal_ids, memories,
+                                                              sequence_length=L, passes=("value", "joint", "baseline"))
+            option_logits, c_out = self._manager_sequence(batch, c_item)
+            new_team_values, new_joint, new_baselines = self.critic.sequence_passes_end(c_out, c_ctx)
+        # PPO clip over the switch decisions (option_mask) inside the loss mask (OCT:515-525)
         n_pol = d_pol if d_pol is not None else mask_flat.sum().clamp_min(1)
         n_term = d_term if d_term is not None else term_mask.sum().clamp_min(1)
         # Categorical(option logits).log_prob(options) and the masked mean option entropy
@@ -176,14 +199,11 @@ class FixedOptionCriticTrainer(TrainerBase):
         next_beta = torch.sigmoid(next_beta_logits)
 
         flat_next_states = next_critic_states.reshape(B * L, N, -1)
-        flat_returns = batch["returns"].reshape(B * L)
-        flat_loss_mask = loss_mask.reshape(B * L)
-        value_loss = trust_region_value_loss(new_team_values, batch["old_team_values"].reshape(B * L), flat_returns,
-                                             current_eps, flat_loss_mask, denom=d_mask)
-        joint_loss = trust_region_value_loss(new_joint, batch["old_joint_option_values"].reshape(B * L),
-                                             flat_returns, current_eps, flat_loss_mask, denom=d_mask)
-        baseline_loss = trust_region_value_loss(new_baselines, batch["old_baselines"].reshape(-1), flat_returns,
-                                                current_eps, flat_loss_mask, denom=d_mask)
+        if side is None:
+            value_loss, joint_loss, baseline_loss = self._value_losses(batch, new_team_values, new_joint, new_baselines,
+                                                                       flat_returns, flat_loss_mask, current_eps, d_mask)
+        else:
+            value_loss, joint_loss, baseline_loss = side_losses
 
         # termination theorem at s': continuation = collective Q(s', omega); reselection =
         # the focal robot's alternatives under its selector, peers fixed (OCT:610-639)
@@ -201,8 +221,23 @@ class FixedOptionCriticTrainer(TrainerBase):
         termination_entropy = (Bernoulli(validate_args=False, logits=next_beta_logits).entropy() * term_mask).sum() / n_term
         mean_beta = (next_beta * term_mask).sum().detach() / n_term
         mean_option_advantage = (option_advantage * term_mask).sum() / n_term
+        if side is not None:
+            main.wait_stream(side)   # the total loss is formed on this stream
         return (policy_loss, value_loss, joint_loss, baseline_loss, termination_loss, option_entropy,
                 termination_entropy, mean_beta, mean_option_advantage)
+
+    @staticmethod
+    def _value_losses(batch, new_team_values, new_joint, new_baselines, flat_returns, flat_loss_mask, current_eps,
+                      d_mask):
+        """The critic's three trust-region value losses (OCT:646-660)."""
+        B_L = flat_returns.shape[0]
+        value_loss = trust_region_value_loss(new_team_values, batch["old_team_values"].reshape(B_L), flat_returns,
+                                             current_eps, flat_loss_mask, denom=d_mask)
+        joint_loss = trust_region_value_loss(new_joint, batch["old_joint_option_values"].reshape(B_L),
+                                             flat_returns, current_eps, flat_loss_mask, denom=d_mask)
+        baseline_loss = trust_region_value_loss(new_baselines, batch["old_baselines"].reshape(-1), flat_returns,
+                                                current_eps, flat_loss_mask, denom=d_mask)
+        return value_loss, joint_loss, baseline_loss
 
     def compute_losses(self, batch: dict, current_eps: float):
         return self._compute_sequence_losses(batch, current_eps)

@@ -47,6 +47,10 @@ _stack_obs = stack_obs
 class POCATrainer(TrainerBase):
     """End-to-end POCA training loop (poca_trainer.py:198-1123)."""
 
+    # the critic's passes on a side stream measured at C3: 1.50 vs 1.48 ms per optimizer step (its LSTM
+    # then leaves the actor's launch), so off by default (SWARM_CRITIC_STREAM=1 turns it on)
+    SIDE_STREAM_DEFAULT = False
+
     algo = "POCA"
     ckpt_prefix = "poca"
 
@@ -184,28 +188,52 @@ class POCATrainer(TrainerBase):
         flat_actions = batch["critic_actions"].reshape(B * L, N, batch["critic_actions"].shape[-1])
         critic_act = self._encode_actions_for_critic(flat_actions)
         focal_ids = batch["focal_agent_ids"].unsqueeze(1).expand(B, L).reshape(-1)
-        # critic_pass and focal_baselines (PT:748-770) as one batched pass (POCACritic.sequence_passes),
-        # whose memory runs in the same LSTM launch as the actor's (lstm_sequences)
-        c_item, c_ctx = self.critic.sequence_passes_begin(
-            flat_states, critic_act, focal_ids,
-            {"value": (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
-             "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
-                          batch["baseline_memory_c"].unsqueeze(0).detach())},
-            sequence_length=L, passes=("value", "baseline"))
-        logits, act, c_out = self._actor_sequence(batch, c_item)
-        new_tv, new_bl = self.critic.sequence_passes_end(c_out, c_ctx)
+        memories = {"value": (batch["critic_memory_h"].unsqueeze(0).detach(), batch["critic_memory_c"].unsqueeze(0).detach()),
+                    "baseline": (batch["baseline_memory_h"].unsqueeze(0).detach(),
+                                 batch["baseline_memory_c"].unsqueeze(0).detach())}
         (d_mask,) = self._denominators([loss_mask.sum()])
+        flat_mask = loss_mask.reshape(B * L)
+        side = self._side_stream()
+        if side is not None:
+            # the critic's branch (its passes, LSTM and value losses) on the side stream, beside the
+            # actor's sequence (TrainerBase._side_stream); its inputs stay referenced until the
+            # backward has been issued
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            self._side_keep = [flat_states, critic_act, focal_ids, flat_mask, batch, memories]
+            with torch.cuda.stream(side):
+                c_item, c_ctx = self.critic.sequence_passes_begin(flat_states, critic_act, focal_ids, memories,
+                                                                  sequence_length=L, passes=("value", "baseline"))
+                c_out = lstm_sequences([c_item])[0][0] if c_item is not None else None
+                new_tv, new_bl = self.critic.sequence_passes_end(c_out, c_ctx)
+                value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
+                                                     batch["returns"].reshape(B * L), current_eps, flat_mask,
+                                                     denom=d_mask)
+                baseline_loss = trust_region_value_loss(new_bl, batch["old_baselines"].reshape(B * L),
+                                                        batch["returns"].reshape(B * L), current_eps, flat_mask,
+                                                        denom=d_mask)
+            logits, act, _ = self._actor_sequence(batch)
+        else:
+            # critic_pass and focal_baselines (PT:748-770) as one batched pass (POCACritic.sequence_passes),
+            # whose memory runs in the same LSTM launch as the actor's (lstm_sequences)
+            c_item, c_ctx = self.critic.sequence_passes_begin(flat_states, critic_act, focal_ids, memories,
+                                                              sequence_length=L, passes=("value", "baseline"))
+            logits, act, c_out = self._actor_sequence(batch, c_item)
+            new_tv, new_bl = self.critic.sequence_passes_end(c_out, c_ctx)
         # Categorical(logits).log_prob(actions) and the masked mean entropy (PT:724-745)
         logp, mean_entropy = categorical_terms(logits, act, loss_mask.reshape(-1), d_mask)
         policy_loss = trust_region_policy_loss(batch["advantages"].unsqueeze(-1).reshape(-1, 1),
                                                logp.reshape(-1, 1),
                                                batch["old_log_probs"].reshape(-1, batch["old_log_probs"].shape[-1]),
                                                current_eps, loss_mask.reshape(-1), denom=d_mask)
-        flat_mask = loss_mask.reshape(B * L)
-        value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
-                                             batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)
-        baseline_loss = trust_region_value_loss(new_bl, batch["old_baselines"].reshape(B * L),
-                                                batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)
+        if side is None:
+            value_loss = trust_region_value_loss(new_tv, batch["old_team_values"].reshape(B * L),
+                                                 batch["returns"].reshape(B * L), current_eps, flat_mask, denom=d_mask)
+            baseline_loss = trust_region_value_loss(new_bl, batch["old_baselines"].reshape(B * L),
+                                                    batch["returns"].reshape(B * L), current_eps, flat_mask,
+                                                    denom=d_mask)
+        else:
+            main.wait_stream(side)   # the total loss is formed on this stream
         return policy_loss, value_loss, baseline_loss, mean_entropy
 
     def compute_losses(self, batch: dict, current_eps: float):
