@@ -40,6 +40,10 @@ _KERNEL_INITS = {
 # rows from which a layer's weight gradient is split over row chunks (A/B: profiles/r04/train/splitk_rows_ab.txt)
 SPLITK_MIN_ROWS = int(os.environ.get("SWARM_SPLITK_MIN_ROWS", "4096"))
 SPLITK_CHUNK_ROWS = int(os.environ.get("SWARM_SPLITK_CHUNK_ROWS", "1024"))   # rows per chunk of that split
+# rows per chunk when the layer's input or output is at most 16 wide (the entity embeddings' 5 / 11
+# inputs, a value head's 1 output): each chunk's product is one small tile, so shorter chunks give
+# the batched GEMM more tiles for the same work (0: SPLITK_CHUNK_ROWS for every layer)
+SPLITK_NARROW_ROWS = int(os.environ.get("SWARM_SPLITK_NARROW_ROWS", "0"))
 SPLITK_SLAB_ROWS = 256     # rows per column-sum slab of its bias gradient
 # False (or SWARM_SPLITK_SUMS=0): the chunk / bias sums run torch's reductions
 SPLITK_NATIVE_SUMS = os.environ.get("SWARM_SPLITK_SUMS", "1") != "0"
@@ -71,10 +75,13 @@ def _split_rows_weight_grad(dy, x, has_bias: bool):
     """(dy^T x, column sums of dy or None) over R >= SPLITK_CHUNK_ROWS rows as _SplitKLinear
     computes its weight gradient: one batched GEMM over row chunks, then the chunk sums."""
     R = x.shape[0]
-    c = R // SPLITK_CHUNK_ROWS
+    out_f = dy.shape[1]
+    chunk = SPLITK_CHUNK_ROWS
+    if SPLITK_NARROW_ROWS > 0 and min(x.shape[1], out_f) <= 16:
+        chunk = SPLITK_NARROW_ROWS
+    c = R // chunk
     L = R // c
     main = c * L
-    out_f = dy.shape[1]
     dyc = dy[:main].view(c, L, out_f)
     parts = torch.bmm(dyc.transpose(1, 2), x[:main].view(c, L, x.shape[1]))
     if SPLITK_NATIVE_SUMS and dy.is_cuda and out_f % 4 == 0 and out_f <= 1024:
