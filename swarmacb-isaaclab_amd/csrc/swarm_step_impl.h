@@ -43,14 +43,6 @@
 #define SWARM_MIN_WAVES_PER_SIMD 4
 #endif
 
-// 1: the disc rays' pre-test runs on rays in pairs with packed fp32 (v_pk_mul_f32 / v_pk_add_f32:
-// the same IEEE products and sums as the scalar code, two rays per instruction), and the wave
-// skips a pair no lane can hit instead of a single ray (a ray without a hit adds max(p, 0) = p)
-#ifndef SWARM_PK_DISC
-#define SWARM_PK_DISC 0
-#endif
-typedef float swarm_f32x2 __attribute__((ext_vector_type(2)));
-
 // Work the wave skips without changing a result (rounds 2-4; the measured
 // alternatives live in git history and profiles/):
 //  * wave-uniform pre-filters skip arena-wall faces and "strictly inside" tests no lane can need;
@@ -793,31 +785,6 @@ __device__ __forceinline__ void proximity_partial(const Geom& g, const Lane& L, 
     // other robots: exact ray-disc hits; only pairs closer than sqrt(0.135^2+0.035^2)
     auto disc = [&](float dx, float dy) {
         const float dsq = dx * dx + dy * dy;
-#if SWARM_PK_DISC
-#pragma unroll
-        for (int k = 0; k < 8; k += 2) {
-            const swarm_f32x2 rx = {rdx[k], rdx[k + 1]}, ry = {rdy[k], rdy[k + 1]};
-            const swarm_f32x2 dx2 = {dx, dx}, dy2 = {dy, dy}, dsq2 = {dsq, dsq};
-            const swarm_f32x2 pa = rx * dx2, pb = ry * dy2;
-            const swarm_f32x2 proj = pa + pb;
-            const swarm_f32x2 pp = proj * proj;
-            const swarm_f32x2 csq = dsq2 - pp;
-            const bool pre0 = (proj.x > 0.0f) & (csq.x <= g.r2);
-            const bool pre1 = (proj.y > 0.0f) & (csq.y <= g.r2);
-            if (!__any(pre0 | pre1)) continue;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float pj = h ? proj.y : proj.x, cs = h ? csq.y : csq.x;
-                const bool pre = h ? pre1 : pre0;
-                const float hc = fsqrt(fmaxf(g.r2 - cs, 0.0f));
-                const float hd = fmaxf(pj - hc, 0.0f);
-                const bool hit = pre & (hd <= g.prox_range);
-                const float rv = clampf(1.0f - hd * g.inv_prox_range, 0.0f, 1.0f);
-                prox[k + h] = fmaxf(prox[k + h], hit ? rv : 0.0f);
-            }
-        }
-        return;
-#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const float proj = rdx[k] * dx + rdy[k] * dy;
